@@ -1,0 +1,114 @@
+/*
+ * jwave_hip.h -- C-ABI of the MI355X (gfx950) JWave-Pro hot-path engine.
+ *
+ * This is the drop-in boundary: a JNI shim binds exactly these entry
+ * points from Java subclasses of JWave-Pro's own transforms.  Plain pointers and sizes
+ * only; all buffers are caller-owned, row-major, batch-major.  Citations are relative to
+ * the reference's src/main/java/jwave/.
+ *
+ * Status codes mirror the reference's exception classes so the glue can rethrow the
+ * exact Java type with jw_last_error()'s message:
+ *   JW_ERR_ILLEGAL_ARGUMENT -> java.lang.IllegalArgumentException (unchecked)
+ *   JW_ERR_FAILURE          -> jwave.exceptions.JWaveFailure      (checked)
+ *
+ * Threading: plans are immutable after creation and may be shared by any number of host
+ * threads (the reference's MODWTThreadSafetyTest pattern).  Every call is reentrant; the
+ * only global state is a thread-local error message.
+ */
+#ifndef JWAVE_HIP_H
+#define JWAVE_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---- */
+#define JW_OK 0
+#define JW_ERR_ILLEGAL_ARGUMENT (-1) /* IllegalArgumentException */
+#define JW_ERR_FAILURE (-2)          /* JWaveFailure */
+#define JW_ERR_DEVICE (-3)           /* HIP runtime / kernel launch error */
+#define JW_ERR_NO_MEMORY (-4)
+#define JW_ERR_UNSUPPORTED (-5)
+
+/* ---- where the caller's buffers live ---- */
+#define JW_HOST 0   /* host memory: the call stages through HBM and synchronises */
+#define JW_DEVICE 1 /* HBM pointers; work is enqueued on `stream` (hipStream_t), async */
+
+/* ---- MODWTTransform.ConvolutionMethod (MODWTTransform.java:149-153) ---- */
+#define JW_CONV_AUTO 0
+#define JW_CONV_DIRECT 1
+#define JW_CONV_FFT 2
+
+/* ---- arithmetic contract ---- */
+#define JW_ARITH_STRICT 0 /* Java operation order, no FMA contraction: bit-identical to the JVM */
+#define JW_ARITH_FMA 1    /* same tap order, fused multiply-add: <= 1e-15 normwise from STRICT */
+
+/* Thread-local text of the last error on this thread (exact reference message where the
+ * reference defines one).  Never NULL. */
+const char* jw_last_error(void);
+
+/* Library version string and the gfx target it was built for. */
+const char* jw_version(void);
+
+/* ======================================================================
+ * MODWT  (replaces MODWTTransform.forwardMODWT :256 / inverseMODWT :337)
+ * ====================================================================== */
+typedef struct jw_modwt_plan jw_modwt_plan;
+
+/* new MODWTTransform(wavelet[, fftThreshold]) (MODWTTransform.java:180-195) followed by
+ * initializeFilterCache (:452-484): normalises the wavelet's scaling/wavelet
+ * decomposition filters (Wavelet.getScalingDeComposition/getWaveletDeComposition) to unit
+ * energy and divides by sqrt(2).  L in [1, 64].  arith: JW_ARITH_*. */
+int jw_modwt_plan_create(jw_modwt_plan** plan, const double* scaling_dec,
+                         const double* wavelet_dec, int L, int fft_threshold, int arith);
+void jw_modwt_plan_destroy(jw_modwt_plan* plan);
+/* The cached base filters g (scaling) and h (wavelet), L each. */
+int jw_modwt_plan_filters(const jw_modwt_plan* plan, double* g, double* h);
+
+/* forwardMODWT(data, levels) for `batch` independent signals of length n.
+ * x: batch x n.  coeffs: batch x (levels+1) x n = [W_1..W_J, V_J] per signal.
+ * Validation order and messages follow MODWTTransform.java:257-282; n == 0 is a no-op.
+ * method: JW_CONV_* (the Java object's setConvolutionMethod state, passed per call). */
+int jw_modwt_forward(const jw_modwt_plan* plan, const double* x, double* coeffs, long n,
+                     int levels, int batch, int method, int where, void* stream);
+/* inverseMODWT(coefficients) (:337-375): coeffs batch x (levels+1) x n -> x batch x n. */
+int jw_modwt_inverse(const jw_modwt_plan* plan, const double* coeffs, double* x, long n,
+                     int levels, int batch, int method, int where, void* stream);
+
+/* ======================================================================
+ * FWT  (replaces FastWaveletTransform.forward/reverse(double[], level) :71/:119,
+ *       the 1-D kernel Wavelet.forward/reverse :236/:277, and the 2-D
+ *       BasicTransform.forward/reverse(double[][], lvlM, lvlN) :361/:436)
+ * ====================================================================== */
+typedef struct jw_fwt_plan jw_fwt_plan;
+
+#define JW_WAVELET_GENERIC 0   /* Wavelet.reverse as written (Wavelet.java:277-303) */
+#define JW_WAVELET_HAAR_ORTH 1 /* Haar1Orthogonal.reverse: contribution x 0.5 (:175-207) */
+
+/* Filters as the Wavelet object holds them (_scalingDeCom, _waveletDeCom, _scalingReCon,
+ * _waveletReCon), motherWavelength M in [1, 64], transformWavelength tw >= 1. */
+int jw_fwt_plan_create(jw_fwt_plan** plan, const double* scaling_dec, const double* wavelet_dec,
+                       const double* scaling_rec, const double* wavelet_rec, int M,
+                       int transform_wavelength, int kind, int arith);
+void jw_fwt_plan_destroy(jw_fwt_plan* plan);
+/* y = forward(x, level) for batch signals of length n (n must be 2^p). */
+int jw_fwt_forward(const jw_fwt_plan* plan, const double* x, double* y, long n, int level,
+                   int batch, int where, void* stream);
+int jw_fwt_reverse(const jw_fwt_plan* plan, const double* y, double* x, long n, int level,
+                   int batch, int where, void* stream);
+/* 2-D: rows with lvlN then columns with lvlM (reverse: columns, then rows). */
+int jw_fwt2d_forward(const jw_fwt_plan* plan, const double* x, double* y, int rows, int cols,
+                     int lvlM, int lvlN, int batch, int where, void* stream);
+int jw_fwt2d_reverse(const jw_fwt_plan* plan, const double* y, double* x, int rows, int cols,
+                     int lvlM, int lvlN, int batch, int where, void* stream);
+
+/* ======================================================================
+ * Synthetic input (bench / tests): java.util.Random(seed0 + b).nextDouble()*2-1 for
+ * signal b, generated in HBM with LCG jump-ahead.  Identical to the oracle's stream.
+ * ====================================================================== */
+int jw_synth_uniform(double* x_dev, long n, int batch, long seed0, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JWAVE_HIP_H */

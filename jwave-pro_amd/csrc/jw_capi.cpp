@@ -1,0 +1,339 @@
+// jw_capi.cpp -- the extern "C" boundary (include/jwave_hip.h): argument validation with the
+// reference's exception classes and messages, plan objects, host<->HBM staging.
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+
+#include "jw_internal.hpp"
+
+namespace jw {
+
+static thread_local char g_err[1024] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+void clear_error() { g_err[0] = '\0'; }
+
+namespace {
+
+// floor(log2 n) as the reference computes it for ints: 31 - numberOfLeadingZeros(N)
+// (MODWTTransform.java:278).
+int floor_log2(long n) {
+  int e = -1;
+  while (n > 0) {
+    n >>= 1;
+    ++e;
+  }
+  return e;
+}
+
+bool is_binary(long n) { return n > 0 && (n & (n - 1)) == 0; }  // MathToolKit.isBinary :185-188
+
+// RAII staging of caller host buffers through HBM (JW_HOST).
+struct DevBuf {
+  double* p = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+int stage_in(DevBuf& d, const double* host, size_t n) {
+  if (n == 0) return JW_OK;
+  JW_HIP_TRY(hipMalloc((void**)&d.p, n * sizeof(double)));
+  if (host) JW_HIP_TRY(hipMemcpy(d.p, host, n * sizeof(double), hipMemcpyHostToDevice));
+  return JW_OK;
+}
+
+int check_where(int where) {
+  if (where != JW_HOST && where != JW_DEVICE)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "where must be JW_HOST (0) or JW_DEVICE (1), got %d",
+                where);
+  return JW_OK;
+}
+
+template <class F>
+int run(int where, void* stream, const double* in, size_t nin, double* out, size_t nout, F&& f) {
+  hipStream_t s = (hipStream_t)stream;
+  if (where == JW_DEVICE) return f(in, out, s);
+  DevBuf din, dout;
+  int st = stage_in(din, in, nin);
+  if (st != JW_OK) return st;
+  st = stage_in(dout, nullptr, nout);
+  if (st != JW_OK) return st;
+  st = f(din.p, dout.p, s);
+  if (st != JW_OK) return st;
+  JW_HIP_TRY(hipStreamSynchronize(s));
+  if (nout) JW_HIP_TRY(hipMemcpy(out, dout.p, nout * sizeof(double), hipMemcpyDeviceToHost));
+  return JW_OK;
+}
+
+}  // namespace
+}  // namespace jw
+
+using namespace jw;
+
+struct jw_modwt_plan : ModwtPlan {};
+struct jw_fwt_plan : FwtPlan {};
+
+extern "C" {
+
+const char* jw_last_error(void) { return g_err; }
+
+const char* jw_version(void) { return "jwave-pro_amd 0.1.0 (gfx950)"; }
+
+// ---------------------------------------------------------------- MODWT
+int jw_modwt_plan_create(jw_modwt_plan** plan, const double* scaling_dec,
+                         const double* wavelet_dec, int L, int fft_threshold, int arith) {
+  clear_error();
+  if (!plan) return fail(JW_ERR_ILLEGAL_ARGUMENT, "plan pointer is null");
+  *plan = nullptr;
+  if (!scaling_dec || !wavelet_dec) return fail(JW_ERR_ILLEGAL_ARGUMENT, "filter pointer is null");
+  if (L < 1 || L > kMaxTaps)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "filter length must be in [1, %d], got %d", kMaxTaps, L);
+  if (arith != JW_ARITH_STRICT && arith != JW_ARITH_FMA)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "unknown arithmetic mode %d", arith);
+  auto* p = new (std::nothrow) jw_modwt_plan();
+  if (!p) return fail(JW_ERR_NO_MEMORY, "out of host memory");
+  p->L = L;
+  p->fft_threshold = fft_threshold;
+  p->arith = arith;
+  // initializeFilterCache (MODWTTransform.java:462-475) with normalize (:599-606); host code
+  // is compiled with -ffp-contract=off, so this is the JVM's sequence.
+  double gd[kMaxTaps], hd[kMaxTaps];
+  for (int i = 0; i < L; ++i) {
+    gd[i] = scaling_dec[i];
+    hd[i] = wavelet_dec[i];
+  }
+  for (double* f : {gd, hd}) {
+    double energy = 0.0;
+    for (int i = 0; i < L; ++i) energy += f[i] * f[i];
+    const double norm = std::sqrt(energy);
+    if (norm > 1e-12)
+      for (int i = 0; i < L; ++i) f[i] /= norm;
+  }
+  const double scale = std::sqrt(2.0);
+  for (int i = 0; i < L; ++i) {
+    p->g[i] = gd[i] / scale;
+    p->h[i] = hd[i] / scale;
+  }
+  *plan = p;
+  return JW_OK;
+}
+
+void jw_modwt_plan_destroy(jw_modwt_plan* plan) { delete plan; }
+
+int jw_modwt_plan_filters(const jw_modwt_plan* plan, double* g, double* h) {
+  clear_error();
+  if (!plan) return fail(JW_ERR_ILLEGAL_ARGUMENT, "plan is null");
+  for (int i = 0; i < plan->L; ++i) {
+    if (g) g[i] = plan->g[i];
+    if (h) h[i] = plan->h[i];
+  }
+  return JW_OK;
+}
+
+static int modwt_method_check(int method) {
+  if (method == JW_CONV_AUTO || method == JW_CONV_DIRECT) return JW_OK;
+  if (method == JW_CONV_FFT)
+    return fail(JW_ERR_UNSUPPORTED,
+                "MODWT convolution method FFT is not implemented on the device yet");
+  return fail(JW_ERR_ILLEGAL_ARGUMENT, "unknown convolution method %d", method);
+}
+
+int jw_modwt_forward(const jw_modwt_plan* plan, const double* x, double* coeffs, long n,
+                     int levels, int batch, int method, int where, void* stream) {
+  clear_error();
+  if (!plan) return fail(JW_ERR_ILLEGAL_ARGUMENT, "plan is null");
+  // MODWTTransform.forwardMODWT validation order (:257-282).
+  if (levels < 1)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT,
+                "MODWTTransform#forwardMODWT - decomposition level must be at least 1, "
+                "requested: %d",
+                levels);
+  if (levels > kMaxModwtLevel)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT,
+                "MODWTTransform#forwardMODWT - maximum supported decomposition level is %d, "
+                "requested: %d",
+                kMaxModwtLevel, levels);
+  if (n == 0 || batch == 0) return JW_OK;  // empty data -> levels+1 empty rows (:266-273)
+  if (n < 0 || batch < 0)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "negative length %ld or batch %d", n, batch);
+  const int theoretical = floor_log2(n);
+  if (levels > theoretical)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT,
+                "Decomposition level %d exceeds theoretical limit %d for signal length %ld",
+                levels, theoretical, n);
+  int st = modwt_method_check(method);
+  if (st != JW_OK) return st;
+  if (st = check_where(where); st != JW_OK) return st;
+  if (!x || !coeffs) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
+  const size_t nin = (size_t)n * batch, nout = (size_t)n * batch * (levels + 1);
+  return run(where, stream, x, nin, coeffs, nout,
+             [&](const double* dx, double* dc, hipStream_t s) {
+               return modwt_forward_device(*plan, dx, dc, n, levels, batch, s);
+             });
+}
+
+int jw_modwt_inverse(const jw_modwt_plan* plan, const double* coeffs, double* x, long n,
+                     int levels, int batch, int method, int where, void* stream) {
+  clear_error();
+  if (!plan) return fail(JW_ERR_ILLEGAL_ARGUMENT, "plan is null");
+  // inverseMODWT (:337-375): fewer than 2 rows -> empty result; upsample rejects j > 13 (:620).
+  if (levels < 1 || n == 0 || batch == 0) return JW_OK;
+  if (levels > kMaxModwtLevel)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT,
+                "MODWTTransform#upsample - maximum supported decomposition level is %d, "
+                "requested: %d",
+                kMaxModwtLevel, levels);
+  if (n < 0 || batch < 0)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "negative length %ld or batch %d", n, batch);
+  int st = modwt_method_check(method);
+  if (st != JW_OK) return st;
+  if (st = check_where(where); st != JW_OK) return st;
+  if (!x || !coeffs) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
+  const size_t nin = (size_t)n * batch * (levels + 1), nout = (size_t)n * batch;
+  return run(where, stream, coeffs, nin, x, nout,
+             [&](const double* dc, double* dx, hipStream_t s) {
+               return modwt_inverse_device(*plan, dc, dx, n, levels, batch, s);
+             });
+}
+
+// ---------------------------------------------------------------- FWT
+int jw_fwt_plan_create(jw_fwt_plan** plan, const double* scaling_dec, const double* wavelet_dec,
+                       const double* scaling_rec, const double* wavelet_rec, int M,
+                       int transform_wavelength, int kind, int arith) {
+  clear_error();
+  if (!plan) return fail(JW_ERR_ILLEGAL_ARGUMENT, "plan pointer is null");
+  *plan = nullptr;
+  if (!scaling_dec || !wavelet_dec || !scaling_rec || !wavelet_rec)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "filter pointer is null");
+  if (M < 1 || M > kMaxTaps)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "filter length must be in [1, %d], got %d", kMaxTaps, M);
+  if (transform_wavelength < 1)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "transform wavelength must be >= 1, got %d",
+                transform_wavelength);
+  if (kind != JW_WAVELET_GENERIC && kind != JW_WAVELET_HAAR_ORTH)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "unknown wavelet kind %d", kind);
+  if (arith != JW_ARITH_STRICT && arith != JW_ARITH_FMA)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "unknown arithmetic mode %d", arith);
+  auto* p = new (std::nothrow) jw_fwt_plan();
+  if (!p) return fail(JW_ERR_NO_MEMORY, "out of host memory");
+  p->M = M;
+  p->tw = transform_wavelength;
+  p->kind = kind;
+  p->arith = arith;
+  for (int i = 0; i < M; ++i) {
+    p->sD[i] = scaling_dec[i];
+    p->wD[i] = wavelet_dec[i];
+    p->sR[i] = scaling_rec[i];
+    p->wR[i] = wavelet_rec[i];
+  }
+  *plan = p;
+  return JW_OK;
+}
+
+void jw_fwt_plan_destroy(jw_fwt_plan* plan) { delete plan; }
+
+// FastWaveletTransform.forward/reverse validation (FastWaveletTransform.java:74-83, :122-131).
+static int fwt_check(long n, int level, const char* who) {
+  if (!is_binary(n))
+    return fail(JW_ERR_FAILURE,
+                "FastWaveletTransform#%s - given array length is not 2^p | p E N ... = 1, 2, 4, "
+                "8, 16, 32, .. please use the Ancient Egyptian Decomposition for any other array "
+                "length!",
+                who);
+  const int levels = floor_log2(n);
+  if (level < 0 || level > levels)
+    return fail(JW_ERR_FAILURE,
+                "FastWaveletTransform#%s - given level is out of range for given array", who);
+  return JW_OK;
+}
+
+int jw_fwt_forward(const jw_fwt_plan* plan, const double* x, double* y, long n, int level,
+                   int batch, int where, void* stream) {
+  clear_error();
+  if (!plan) return fail(JW_ERR_ILLEGAL_ARGUMENT, "plan is null");
+  int st = fwt_check(n, level, "forward");
+  if (st != JW_OK) return st;
+  if (st = check_where(where); st != JW_OK) return st;
+  if (batch <= 0) return batch == 0 ? JW_OK : fail(JW_ERR_ILLEGAL_ARGUMENT, "negative batch");
+  if (!x || !y) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
+  const size_t elems = (size_t)n * batch;
+  return run(where, stream, x, elems, y, elems, [&](const double* dx, double* dy, hipStream_t s) {
+    return fwt_forward_device(*plan, dx, dy, n, level, batch, s);
+  });
+}
+
+int jw_fwt_reverse(const jw_fwt_plan* plan, const double* y, double* x, long n, int level,
+                   int batch, int where, void* stream) {
+  clear_error();
+  if (!plan) return fail(JW_ERR_ILLEGAL_ARGUMENT, "plan is null");
+  int st = fwt_check(n, level, "reverse");
+  if (st != JW_OK) return st;
+  if (st = check_where(where); st != JW_OK) return st;
+  if (batch <= 0) return batch == 0 ? JW_OK : fail(JW_ERR_ILLEGAL_ARGUMENT, "negative batch");
+  if (!x || !y) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
+  const size_t elems = (size_t)n * batch;
+  return run(where, stream, y, elems, x, elems, [&](const double* dy, double* dx, hipStream_t s) {
+    return fwt_reverse_device(*plan, dy, dx, n, level, batch, s);
+  });
+}
+
+int jw_fwt2d_forward(const jw_fwt_plan* plan, const double* x, double* y, int rows, int cols,
+                     int lvlM, int lvlN, int batch, int where, void* stream) {
+  clear_error();
+  if (!plan) return fail(JW_ERR_ILLEGAL_ARGUMENT, "plan is null");
+  // rows are transformed first (with cols samples, lvlN), then columns (rows samples, lvlM)
+  int st = fwt_check(cols, lvlN, "forward");
+  if (st == JW_OK) st = fwt_check(rows, lvlM, "forward");
+  if (st != JW_OK) return st;
+  if (st = check_where(where); st != JW_OK) return st;
+  if (batch <= 0) return batch == 0 ? JW_OK : fail(JW_ERR_ILLEGAL_ARGUMENT, "negative batch");
+  if (!x || !y) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
+  const size_t elems = (size_t)rows * cols * batch;
+  return run(where, stream, x, elems, y, elems, [&](const double* dx, double* dy, hipStream_t s) {
+    return fwt2d_forward_device(*plan, dx, dy, rows, cols, lvlM, lvlN, batch, s);
+  });
+}
+
+int jw_fwt2d_reverse(const jw_fwt_plan* plan, const double* y, double* x, int rows, int cols,
+                     int lvlM, int lvlN, int batch, int where, void* stream) {
+  clear_error();
+  if (!plan) return fail(JW_ERR_ILLEGAL_ARGUMENT, "plan is null");
+  // columns are transformed first (rows samples, lvlM), then rows (cols samples, lvlN)
+  int st = fwt_check(rows, lvlM, "reverse");
+  if (st == JW_OK) st = fwt_check(cols, lvlN, "reverse");
+  if (st != JW_OK) return st;
+  if (st = check_where(where); st != JW_OK) return st;
+  if (batch <= 0) return batch == 0 ? JW_OK : fail(JW_ERR_ILLEGAL_ARGUMENT, "negative batch");
+  if (!x || !y) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
+  const size_t elems = (size_t)rows * cols * batch;
+  return run(where, stream, y, elems, x, elems, [&](const double* dy, double* dx, hipStream_t s) {
+    return fwt2d_reverse_device(*plan, dy, dx, rows, cols, lvlM, lvlN, batch, s);
+  });
+}
+
+// ---------------------------------------------------------------- synthetic input
+int jw_synth_uniform(double* x_dev, long n, int batch, long seed0, void* stream) {
+  clear_error();
+  if (n < 0 || batch < 0) return fail(JW_ERR_ILLEGAL_ARGUMENT, "negative size");
+  if (n == 0 || batch == 0) return JW_OK;
+  if (!x_dev) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
+  return synth_uniform_device(x_dev, n, batch, seed0, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,71 @@
+// jw_internal.hpp -- shared internals of libjwave_hip.so (not part of the C-ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+#include "jwave_hip.h"
+
+namespace jw {
+
+constexpr int kMaxTaps = 64;      // longest filter a plan accepts (Daubechies20 / Symlet20 = 40)
+constexpr int kMaxModwtLevel = 13;  // MODWTTransform.MAX_DECOMPOSITION_LEVEL (MODWTTransform.java:111)
+
+// Thread-local error text, returned by jw_last_error().
+void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+void clear_error();
+
+#define JW_HIP_TRY(expr)                                                                   \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return ::jw::fail(JW_ERR_DEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                        __FILE__, __LINE__);                                               \
+  } while (0)
+
+// Filter taps passed to kernels by value (lands in SGPRs: wave-uniform).
+struct Taps {
+  double a[kMaxTaps];
+  double b[kMaxTaps];
+};
+
+// MODWT plan = an initialised MODWTTransform (filters cached, MODWTTransform.java:452-484).
+struct ModwtPlan {
+  int L;
+  int fft_threshold;
+  int arith;
+  double g[kMaxTaps];  // g_modwt_base
+  double h[kMaxTaps];  // h_modwt_base
+};
+
+struct FwtPlan {
+  int M;
+  int tw;
+  int kind;
+  int arith;
+  double sD[kMaxTaps], wD[kMaxTaps], sR[kMaxTaps], wR[kMaxTaps];
+};
+
+// ---- launchers (return JW_OK or a JW_ERR_* with the error text set) ----
+int modwt_forward_device(const ModwtPlan& p, const double* x, double* coeffs, long n, int J,
+                         int batch, hipStream_t s);
+int modwt_inverse_device(const ModwtPlan& p, const double* coeffs, double* x, long n, int J,
+                         int batch, hipStream_t s);
+int fwt_forward_device(const FwtPlan& p, const double* x, double* y, long n, int level, int batch,
+                       hipStream_t s);
+int fwt_reverse_device(const FwtPlan& p, const double* y, double* x, long n, int level, int batch,
+                       hipStream_t s);
+int fwt2d_forward_device(const FwtPlan& p, const double* x, double* y, int rows, int cols,
+                         int lvlM, int lvlN, int batch, hipStream_t s);
+int fwt2d_reverse_device(const FwtPlan& p, const double* y, double* x, int rows, int cols,
+                         int lvlM, int lvlN, int batch, hipStream_t s);
+int synth_uniform_device(double* x, long n, int batch, long seed0, hipStream_t s);
+
+// Device workspace that grows on demand (per calling thread, per device).
+double* workspace(size_t doubles, int* status);
+
+}  // namespace jw

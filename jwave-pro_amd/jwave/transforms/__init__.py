@@ -1,0 +1,6 @@
+"""jwave.transforms -- host mirror of the reference's transform classes (hot path only)."""
+from .fwt import BasicTransform, FastWaveletTransform, WaveletTransform
+from .modwt import ConvolutionMethod, MODWTTransform
+
+__all__ = ["BasicTransform", "WaveletTransform", "FastWaveletTransform", "MODWTTransform",
+           "ConvolutionMethod"]

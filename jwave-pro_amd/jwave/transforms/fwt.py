@@ -1,0 +1,165 @@
+"""FWT host mirror: BasicTransform / WaveletTransform / FastWaveletTransform.
+
+Same names, argument meaning and error behaviour as the reference
+(src/main/java/jwave/transforms/BasicTransform.java, WaveletTransform.java:77-182,
+FastWaveletTransform.java:71-153); the cascade itself runs in the HIP engine
+(jw_fwt_* in include/jwave_hip.h).  Extensions beyond the Java API are the batched
+``forwardBatch`` / ``reverseBatch`` / ``forward2DBatch`` / ``reverse2DBatch``.
+"""
+import ctypes
+import math
+
+import numpy as np
+
+from .. import _native
+from .._arrays import as_input
+from ..exceptions import JWaveFailure
+
+
+def _is_binary(n):  # MathToolKit.isBinary :185-188
+    return n > 0 and (n & (n - 1)) == 0
+
+
+def _get_exponent(f):  # MathToolKit.getExponent :202-206: (int)(log f / log 2)
+    return int(math.log(f) / math.log(2.))
+
+
+class BasicTransform:
+    """jwave.transforms.BasicTransform (abstract)."""
+
+    _name = None
+
+    def getName(self):
+        return self._name
+
+    def isBinary(self, number):
+        return _is_binary(number)
+
+    def calcExponent(self, number):  # BasicTransform.java:688-697
+        if not _is_binary(number):
+            raise JWaveFailure("BasicTransform#calcExponent - given number is not binary: "
+                               "2^p | pEN .. = 1, 2, 4, 8, 16, 32, .. ")
+        return _get_exponent(number)
+
+
+class WaveletTransform(BasicTransform):
+    """jwave.transforms.WaveletTransform (abstract, holds the wavelet)."""
+
+    def __init__(self, wavelet):
+        self._wavelet = wavelet
+
+    def getWavelet(self):
+        return self._wavelet
+
+
+class FastWaveletTransform(WaveletTransform):
+    """jwave.transforms.FastWaveletTransform -- the FWT cascade on the MI355X."""
+
+    def __init__(self, wavelet, arith="strict"):
+        super().__init__(wavelet)
+        self._name = "Fast Wavelet Transform"
+        self._arith = _native.JW_ARITH_FMA if arith == "fma" else _native.JW_ARITH_STRICT
+        L = _native.lib()
+        M = wavelet.getMotherWavelength()
+        arrs = [np.ascontiguousarray(f, dtype=np.float64)
+                for f in (wavelet.getScalingDeComposition(), wavelet.getWaveletDeComposition(),
+                          wavelet.getScalingReConstruction(), wavelet.getWaveletReConstruction())]
+        self._plan = ctypes.c_void_p()
+        _native.check(L.jw_fwt_plan_create(ctypes.byref(self._plan),
+                                           *[ctypes.c_void_p(a.ctypes.data) for a in arrs], M,
+                                           wavelet.getTransformWavelength(),
+                                           getattr(wavelet, "kind", 0), self._arith))
+
+    def __del__(self):
+        plan = getattr(self, "_plan", None)
+        if plan and _native._lib is not None:
+            _native._lib.jw_fwt_plan_destroy(plan)
+
+    # ---- 1-D (WaveletTransform.forward/reverse(double[]) :77-112, FWT :71-153) ----
+    def forward(self, arr, level=None, lvlN=None):
+        if lvlN is not None:  # forward(double[][], lvlM, lvlN)
+            return self._forward2d(arr, level, lvlN)
+        a = as_input(arr)
+        if len(a.shape) == 2:  # forward(double[][]) (BasicTransform.java:336-342)
+            return self._forward2d(arr, _get_exponent(a.shape[0]), _get_exponent(a.shape[1]))
+        if level is None:
+            n = a.shape[0]
+            if not _is_binary(n):
+                raise JWaveFailure(
+                    "WaveletTransform#forward - given array length is not 2^p | p E N ... = 1, 2, "
+                    "4, 8, 16, 32, .. please use the Ancient Egyptian Decomposition for any other "
+                    "array length!")
+            level = self.calcExponent(n)
+        return self._run1d(a, level, batch=False, reverse=False)
+
+    def reverse(self, arr, level=None, lvlN=None):
+        if lvlN is not None:
+            return self._reverse2d(arr, level, lvlN)
+        a = as_input(arr)
+        if len(a.shape) == 2:
+            return self._reverse2d(arr, _get_exponent(a.shape[0]), _get_exponent(a.shape[1]))
+        if level is None:
+            n = a.shape[0]
+            if not _is_binary(n):
+                raise JWaveFailure(
+                    "WaveletTransform#reverse - given array length is not 2^p | p E N ... = 1, 2, "
+                    "4, 8, 16, 32, .. please use the Ancient Egyptian Decomposition for any other "
+                    "array length!")
+            level = self.calcExponent(n)
+        return self._run1d(a, level, batch=False, reverse=True)
+
+    def forwardBatch(self, signals, level):
+        """Batched extension: every row of ``signals`` (B x n) with ``level``."""
+        return self._run1d(as_input(signals), level, batch=True, reverse=False)
+
+    def reverseBatch(self, coeffs, level):
+        return self._run1d(as_input(coeffs), level, batch=True, reverse=True)
+
+    def _run1d(self, a, level, batch, reverse):
+        L = _native.lib()
+        n = a.shape[-1]
+        B = a.shape[0] if batch else 1
+        out = a.empty(a.shape)
+        fn = L.jw_fwt_reverse if reverse else L.jw_fwt_forward
+        _native.check(fn(self._plan, a.ptr, out.ptr, n, int(level), B, a.where, a.stream))
+        return out.result()
+
+    # ---- 2-D (BasicTransform.forward/reverse(double[][], lvlM, lvlN) :361-474) ----
+    def _forward2d(self, mat, lvlM, lvlN, batch=False):
+        a = as_input(mat)
+        L = _native.lib()
+        rows, cols = a.shape[-2], a.shape[-1]
+        B = a.shape[0] if batch else 1
+        out = a.empty(a.shape)
+        _native.check(L.jw_fwt2d_forward(self._plan, a.ptr, out.ptr, rows, cols, int(lvlM),
+                                         int(lvlN), B, a.where, a.stream))
+        return out.result()
+
+    def _reverse2d(self, mat, lvlM, lvlN, batch=False):
+        a = as_input(mat)
+        L = _native.lib()
+        rows, cols = a.shape[-2], a.shape[-1]
+        B = a.shape[0] if batch else 1
+        out = a.empty(a.shape)
+        _native.check(L.jw_fwt2d_reverse(self._plan, a.ptr, out.ptr, rows, cols, int(lvlM),
+                                         int(lvlN), B, a.where, a.stream))
+        return out.result()
+
+    def forward2DBatch(self, images, lvlM, lvlN):
+        return self._forward2d(images, lvlM, lvlN, batch=True)
+
+    def reverse2DBatch(self, images, lvlM, lvlN):
+        return self._reverse2d(images, lvlM, lvlN, batch=True)
+
+    # ---- decompose / recompose (WaveletTransform.java:136-182) ----
+    def decompose(self, arrTime):
+        a = np.asarray(arrTime, dtype=np.float64)
+        levels = self.calcExponent(a.shape[0])
+        return np.stack([np.asarray(self.forward(a, p)) for p in range(levels + 1)])
+
+    def recompose(self, matDeComp, level=None):
+        if level is None:
+            level = 0
+        if level < 0 or level >= len(matDeComp):
+            raise JWaveFailure("WaveletTransform#recompose - given level is out of range")
+        return self.reverse(np.asarray(matDeComp[level], dtype=np.float64), level)

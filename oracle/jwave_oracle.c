@@ -1,0 +1,537 @@
+/*
+ * jwave_oracle.c -- TEST INFRASTRUCTURE ONLY (see jwave_oracle.h).
+ *
+ * Operation-for-operation restatement of JWave-Pro's hot path.  Compile with
+ * -O2 -ffp-contract=off (oracle/Makefile): no FMA contraction, left-to-right
+ * evaluation exactly as the Java expressions are written.  Every function cites
+ * the reference lines it follows (paths relative to src/main/java/jwave/).
+ */
+#include "jwave_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define JAVA_PI 3.141592653589793 /* Math.PI */
+
+/* ------------------------------------------------------------------------ */
+/* java.util.Random (JDK 21 java/util/Random.java: constructor, next, nextDouble) */
+/* ------------------------------------------------------------------------ */
+#define LCG_A 0x5DEECE66DULL
+#define LCG_C 0xBULL
+#define LCG_MASK ((1ULL << 48) - 1)
+
+void jwo_random_init(jwo_random* r, int64_t seed) {
+  r->seed = ((uint64_t)seed ^ LCG_A) & LCG_MASK;
+}
+
+int32_t jwo_random_next(jwo_random* r, int bits) {
+  r->seed = (r->seed * LCG_A + LCG_C) & LCG_MASK;
+  return (int32_t)(r->seed >> (48 - bits));
+}
+
+double jwo_random_next_double(jwo_random* r) {
+  int64_t hi = (int64_t)jwo_random_next(r, 26);
+  int64_t lo = (int64_t)jwo_random_next(r, 27);
+  return (double)((hi << 27) + lo) * 0x1.0p-53;
+}
+
+void jwo_fill_uniform(double* out, long n, int64_t seed) {
+  jwo_random r;
+  jwo_random_init(&r, seed);
+  for (long i = 0; i < n; i++) out[i] = jwo_random_next_double(&r) * 2.0 - 1.0;
+}
+
+/* k-step LCG jump: s_k = A^k s + C_k (mod 2^48) by squaring the affine map. */
+static uint64_t lcg_skip(uint64_t s, uint64_t k) {
+  uint64_t a = LCG_A, c = LCG_C, acc_a = 1, acc_c = 0;
+  while (k) {
+    if (k & 1) { acc_a = (acc_a * a) & LCG_MASK; acc_c = (acc_c * a + c) & LCG_MASK; }
+    c = (c * (a + 1)) & LCG_MASK;
+    a = (a * a) & LCG_MASK;
+    k >>= 1;
+  }
+  return (acc_a * s + acc_c) & LCG_MASK;
+}
+
+void jwo_fill_uniform_range(double* out, long start, long count, int64_t seed) {
+  jwo_random r;
+  jwo_random_init(&r, seed);
+  r.seed = lcg_skip(r.seed, 2ULL * (uint64_t)start);
+  for (long i = 0; i < count; i++) out[i] = jwo_random_next_double(&r) * 2.0 - 1.0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* MODWT filters: MODWTTransform.initializeFilterCache :452-484, normalize :599-606 */
+/* ------------------------------------------------------------------------ */
+static void java_normalize(double* f, int L) {
+  double energy = 0.0;
+  for (int i = 0; i < L; i++) energy += f[i] * f[i];
+  double norm = sqrt(energy);
+  if (norm > 1e-12)
+    for (int i = 0; i < L; i++) f[i] /= norm;
+}
+
+void jwo_modwt_filters(const double* scal_dec, const double* wav_dec, int L, double* g, double* h) {
+  double* gd = (double*)malloc(sizeof(double) * L);
+  double* hd = (double*)malloc(sizeof(double) * L);
+  memcpy(gd, scal_dec, sizeof(double) * L);
+  memcpy(hd, wav_dec, sizeof(double) * L);
+  java_normalize(gd, L);
+  java_normalize(hd, L);
+  double scale = sqrt(2.0);
+  for (int i = 0; i < L; i++) {
+    g[i] = gd[i] / scale;
+    h[i] = hd[i] / scale;
+  }
+  free(gd);
+  free(hd);
+}
+
+/* upsample :618-630 -- gap = 2^(level-1)-1 zeros between taps. */
+long jwo_modwt_upsample(const double* base, int L, int level, double* out) {
+  if (level <= 1) {
+    memcpy(out, base, sizeof(double) * L);
+    return L;
+  }
+  long gap = (1L << (level - 1)) - 1;
+  long M = L + (long)(L - 1) * gap;
+  memset(out, 0, sizeof(double) * M);
+  for (int i = 0; i < L; i++) out[i * (gap + 1)] = base[i];
+  return M;
+}
+
+static long floor_mod(long a, long n) { /* Math.floorMod */
+  long r = a % n;
+  return (r != 0 && ((r < 0) != (n < 0))) ? r + n : r;
+}
+
+/* circularConvolve :677-690 (all M taps, zeros included, floorMod). */
+static void circ_conv(const double* s, long N, const double* f, long M, int L, double* out) {
+  (void)L;
+  for (long n = 0; n < N; n++) {
+    double sum = 0.0;
+    for (long m = 0; m < M; m++) sum += s[floor_mod(n - m, N)] * f[m];
+    out[n] = sum;
+  }
+}
+
+/* circularConvolveAdjoint :703-716. */
+static void circ_conv_adj(const double* s, long N, const double* f, long M, int L,
+                          double* out) {
+  (void)L;
+  for (long n = 0; n < N; n++) {
+    double sum = 0.0;
+    for (long m = 0; m < M; m++) sum += s[floor_mod(n + m, N)] * f[m];
+    out[n] = sum;
+  }
+}
+
+int jwo_modwt_auto_uses_fft(long N, long M, int threshold) {
+  int32_t prod = (int32_t)((uint32_t)N * (uint32_t)M); /* Java int multiply wraps */
+  return prod > threshold;
+}
+
+typedef void (*conv_fn)(const double*, long, const double*, long, int, double*);
+
+static void modwt_forward(const double* x, long N, int J, const double* g, const double* h, int L,
+                          double* coeffs, conv_fn conv) {
+  long Mmax = (long)(L - 1) * (1L << (J - 1)) + 1;
+  double* gu = (double*)malloc(sizeof(double) * Mmax);
+  double* hu = (double*)malloc(sizeof(double) * Mmax);
+  double* v = (double*)malloc(sizeof(double) * N);
+  memcpy(v, x, sizeof(double) * N); /* vCurrent = copyOf(data) :288 */
+  for (int j = 1; j <= J; j++) {    /* :290-304 */
+    long M = jwo_modwt_upsample(g, L, j, gu);
+    jwo_modwt_upsample(h, L, j, hu);
+    conv(v, N, hu, M, L, coeffs + (long)(j - 1) * N); /* W_j */
+    conv(v, N, gu, M, L, coeffs + (long)J * N);       /* V_j */
+    memcpy(v, coeffs + (long)J * N, sizeof(double) * N);
+  }
+  free(gu); free(hu); free(v);
+}
+
+static void modwt_inverse(const double* coeffs, long N, int J, const double* g, const double* h,
+                          int L, double* x, conv_fn conv_adj) {
+  long Mmax = (long)(L - 1) * (1L << (J - 1)) + 1;
+  double* gu = (double*)malloc(sizeof(double) * Mmax);
+  double* hu = (double*)malloc(sizeof(double) * Mmax);
+  double* va = (double*)malloc(sizeof(double) * N);
+  double* vd = (double*)malloc(sizeof(double) * N);
+  memcpy(x, coeffs + (long)J * N, sizeof(double) * N); /* :353 */
+  for (int j = J; j >= 1; j--) {                        /* :355-372 */
+    long M = jwo_modwt_upsample(g, L, j, gu);
+    jwo_modwt_upsample(h, L, j, hu);
+    conv_adj(x, N, gu, M, L, va);
+    conv_adj(coeffs + (long)(j - 1) * N, N, hu, M, L, vd);
+    for (long i = 0; i < N; i++) x[i] = va[i] + vd[i];
+  }
+  free(gu); free(hu); free(va); free(vd);
+}
+
+/* Same sums with the up-sampled zero taps skipped (x*0 = +-0 added to a running sum that is
+ * never -0.0 leaves it bit-identical for finite x); tests pin it to the faithful version. */
+static void circ_conv_nz_impl(const double* s, long N, const double* f, long M, int L,
+                              double* out, int adj) {
+  const long d = L > 1 ? (M - 1) / (L - 1) : 1; /* M = (L-1)*2^(j-1) + 1 */
+  for (long n = 0; n < N; n++) {
+    double sum = 0.0;
+    for (int k = 0; k < L; k++) {
+      long m = (long)k * d;
+      sum += s[floor_mod(adj ? n + m : n - m, N)] * f[m];
+    }
+    out[n] = sum;
+  }
+}
+static void circ_conv_nz(const double* s, long N, const double* f, long M, int L, double* out) {
+  circ_conv_nz_impl(s, N, f, M, L, out, 0);
+}
+static void circ_conv_adj_nz(const double* s, long N, const double* f, long M, int L,
+                             double* out) {
+  circ_conv_nz_impl(s, N, f, M, L, out, 1);
+}
+
+void jwo_modwt_forward_direct_nz(const double* x, long N, int J, const double* g,
+                                 const double* h, int L, double* coeffs) {
+  modwt_forward(x, N, J, g, h, L, coeffs, circ_conv_nz);
+}
+
+void jwo_modwt_inverse_direct_nz(const double* coeffs, long N, int J, const double* g,
+                                 const double* h, int L, double* x) {
+  modwt_inverse(coeffs, N, J, g, h, L, x, circ_conv_adj_nz);
+}
+
+void jwo_modwt_forward_direct(const double* x, long N, int J, const double* g, const double* h,
+                              int L, double* coeffs) {
+  modwt_forward(x, N, J, g, h, L, coeffs, circ_conv);
+}
+
+void jwo_modwt_inverse_direct(const double* coeffs, long N, int J, const double* g,
+                              const double* h, int L, double* x) {
+  modwt_inverse(coeffs, N, J, g, h, L, x, circ_conv_adj);
+}
+
+/* ------------------------------------------------------------------------ */
+/* FFT: FastFourierTransform.java forward/reverse :112-164, fftCooleyTukey :172-212,   */
+/* fftCooleyTukeyInternal (no 1/n), fftBluestein :259-324.  Complex.mul :286-288.      */
+/* ------------------------------------------------------------------------ */
+static void fft_ct(double* x, long n, int inverse, int normalize) {
+  int p = 0;
+  while ((1L << p) < n) p++;
+  for (long k = 0; k < n; k++) { /* bit reversal :176-184 */
+    long j = 0;
+    for (int b = 0; b < p; b++) j |= ((k >> b) & 1L) << (p - 1 - b);
+    if (j > k) {
+      double tr = x[2 * j], ti = x[2 * j + 1];
+      x[2 * j] = x[2 * k]; x[2 * j + 1] = x[2 * k + 1];
+      x[2 * k] = tr; x[2 * k + 1] = ti;
+    }
+  }
+  for (long size = 2; size <= n; size *= 2) { /* :188-202 */
+    double angle = 2 * JAVA_PI / (double)size * (inverse ? 1 : -1);
+    double wr = cos(angle), wi = sin(angle);
+    long half = size / 2;
+    for (long start = 0; start < n; start += size) {
+      double nr = 1, ni = 0; /* wn = (1,0) */
+      for (long k = 0; k < half; k++) {
+        double* u = x + 2 * (start + k);
+        double* v = x + 2 * (start + k + half);
+        double ur = u[0], ui = u[1];
+        double tr = nr * v[0] - ni * v[1]; /* t = wn.mul(x[..]) */
+        double ti = nr * v[1] + ni * v[0];
+        u[0] = ur + tr; u[1] = ui + ti;
+        v[0] = ur - tr; v[1] = ui - ti;
+        double nnr = nr * wr - ni * wi; /* wn = wn.mul(w) */
+        double nni = nr * wi + ni * wr;
+        nr = nnr; ni = nni;
+      }
+    }
+  }
+  if (inverse && normalize) { /* :207-211  x[i].mul(1.0/n) */
+    double s = 1.0 / (double)n;
+    for (long i = 0; i < n; i++) { x[2 * i] *= s; x[2 * i + 1] *= s; }
+  }
+}
+
+static void fft_bluestein(double* x, long n, int inverse) {
+  long m = 1;
+  while (m < 2 * n - 1) m *= 2;
+  double* chirp = (double*)malloc(sizeof(double) * 2 * n);
+  double* a = (double*)calloc(2 * m, sizeof(double));
+  double* b = (double*)calloc(2 * m, sizeof(double));
+  for (long i = 0; i < n; i++) {
+    double angle = JAVA_PI * (double)i * (double)i / (double)n * (inverse ? 1 : -1);
+    chirp[2 * i] = cos(angle);
+    chirp[2 * i + 1] = sin(angle);
+  }
+  for (long i = 0; i < n; i++) { /* a[i] = x[i].mul(chirp[i]) */
+    double xr = x[2 * i], xi = x[2 * i + 1], cr = chirp[2 * i], ci = chirp[2 * i + 1];
+    a[2 * i] = xr * cr - xi * ci;
+    a[2 * i + 1] = xr * ci + xi * cr;
+  }
+  b[0] = chirp[0]; b[1] = -chirp[1];
+  for (long i = 1; i < n; i++) {
+    b[2 * i] = chirp[2 * i]; b[2 * i + 1] = -chirp[2 * i + 1];
+    b[2 * (m - i)] = chirp[2 * i]; b[2 * (m - i) + 1] = -chirp[2 * i + 1];
+  }
+  fft_ct(a, m, 0, 0);
+  fft_ct(b, m, 0, 0);
+  for (long i = 0; i < m; i++) {
+    double ar = a[2 * i], ai = a[2 * i + 1], br = b[2 * i], bi = b[2 * i + 1];
+    a[2 * i] = ar * br - ai * bi;
+    a[2 * i + 1] = ar * bi + ai * br;
+  }
+  fft_ct(a, m, 1, 0);
+  double sm = 1.0 / (double)m;
+  for (long i = 0; i < m; i++) { a[2 * i] *= sm; a[2 * i + 1] *= sm; }
+  double sn = 1.0 / (double)n;
+  for (long i = 0; i < n; i++) {
+    double ar = a[2 * i], ai = a[2 * i + 1], cr = chirp[2 * i], ci = chirp[2 * i + 1];
+    double rr = ar * cr - ai * ci, ri = ar * ci + ai * cr;
+    if (inverse) { rr *= sn; ri *= sn; }
+    x[2 * i] = rr; x[2 * i + 1] = ri;
+  }
+  free(chirp); free(a); free(b);
+}
+
+void jwo_fft(double* reim, long n, int inverse) {
+  if (n <= 1) return;
+  if ((n & (n - 1)) == 0) fft_ct(reim, n, inverse, 1);
+  else fft_bluestein(reim, n, inverse);
+}
+
+/* wrapFilterToSignalLength :729-741 */
+static void wrap_filter(const double* f, long M, long N, double* p) {
+  memset(p, 0, sizeof(double) * N);
+  for (long i = 0; i < M; i++) p[i % N] += f[i];
+}
+
+/* circularConvolveFFT :752-786 and circularConvolveFFTAdjoint :798-837 */
+static void fft_conv_impl(const double* s, long N, const double* f, long M, double* out, int adj) {
+  double* sc = (double*)malloc(sizeof(double) * 2 * N);
+  double* fc = (double*)malloc(sizeof(double) * 2 * N);
+  double* p = (double*)malloc(sizeof(double) * N);
+  wrap_filter(f, M, N, p);
+  for (long i = 0; i < N; i++) {
+    sc[2 * i] = s[i]; sc[2 * i + 1] = 0;
+    fc[2 * i] = p[i]; fc[2 * i + 1] = 0;
+  }
+  jwo_fft(sc, N, 0);
+  jwo_fft(fc, N, 0);
+  for (long i = 0; i < N; i++) {
+    double sr = sc[2 * i], si = sc[2 * i + 1], fr = fc[2 * i], fi = fc[2 * i + 1];
+    if (adj) fi = -fi; /* filterFFT[i].conjugate() */
+    sc[2 * i] = sr * fr - si * fi;
+    sc[2 * i + 1] = sr * fi + si * fr;
+  }
+  jwo_fft(sc, N, 1);
+  for (long i = 0; i < N; i++) out[i] = sc[2 * i];
+  free(sc); free(fc); free(p);
+}
+static void fft_conv(const double* s, long N, const double* f, long M, int L, double* out) {
+  (void)L;
+  fft_conv_impl(s, N, f, M, out, 0);
+}
+static void fft_conv_adj(const double* s, long N, const double* f, long M, int L, double* out) {
+  (void)L;
+  fft_conv_impl(s, N, f, M, out, 1);
+}
+
+void jwo_modwt_forward_fft(const double* x, long N, int J, const double* g, const double* h,
+                           int L, double* coeffs) {
+  modwt_forward(x, N, J, g, h, L, coeffs, fft_conv);
+}
+
+void jwo_modwt_inverse_fft(const double* coeffs, long N, int J, const double* g,
+                           const double* h, int L, double* x) {
+  modwt_inverse(coeffs, N, J, g, h, L, x, fft_conv_adj);
+}
+
+/* ------------------------------------------------------------------------ */
+/* FWT: Wavelet.forward :236-260, Wavelet.reverse :277-303,                           */
+/* Haar1Orthogonal.reverse :175-207 (x0.5), FastWaveletTransform.forward/reverse :71-153 */
+/* ------------------------------------------------------------------------ */
+void jwo_wavelet_forward(const double* in, int len, const double* sD, const double* wD, int M,
+                         double* out) {
+  int h = len >> 1;
+  for (int i = 0; i < h; i++) {
+    out[i] = out[i + h] = 0.;
+    for (int j = 0; j < M; j++) {
+      int k = (i << 1) + j;
+      while (k >= len) k -= len;
+      out[i] += in[k] * sD[j];
+      out[i + h] += in[k] * wD[j];
+    }
+  }
+}
+
+void jwo_wavelet_reverse(const double* in, int len, const double* sR, const double* wR, int M,
+                         int kind, double* out) {
+  for (int i = 0; i < len; i++) out[i] = 0.;
+  int h = len >> 1;
+  for (int i = 0; i < h; i++) {
+    for (int j = 0; j < M; j++) {
+      int k = (i << 1) + j;
+      while (k >= len) k -= len;
+      if (kind == 1)
+        out[k] += .5 * ((in[i] * sR[j]) + (in[i + h] * wR[j]));
+      else
+        out[k] += (in[i] * sR[j]) + (in[i + h] * wR[j]);
+    }
+  }
+}
+
+static int java_get_exponent(double f) { /* MathToolKit.getExponent :202-206 */
+  return (int)(log(f) / log(2.));
+}
+
+void jwo_fwt_forward(const double* x, long n, int level, const double* sD, const double* wD,
+                     int M, int tw, double* y) {
+  double* tmp = (double*)malloc(sizeof(double) * (n > 0 ? n : 1));
+  memcpy(y, x, sizeof(double) * n);
+  int l = 0;
+  long h = n;
+  while (h >= tw && l < level) {
+    jwo_wavelet_forward(y, (int)h, sD, wD, M, tmp);
+    memcpy(y, tmp, sizeof(double) * h);
+    h = h >> 1;
+    l++;
+  }
+  free(tmp);
+}
+
+void jwo_fwt_reverse(const double* y, long n, int level, const double* sR, const double* wR,
+                     int M, int tw, int kind, double* x) {
+  double* tmp = (double*)malloc(sizeof(double) * (n > 0 ? n : 1));
+  memcpy(x, y, sizeof(double) * n);
+  long h = tw;
+  int steps = java_get_exponent((double)n);
+  for (int l = level; l < steps; l++) h = h << 1;
+  while (h <= n && h >= tw) {
+    jwo_wavelet_reverse(x, (int)h, sR, wR, M, kind, tmp);
+    memcpy(x, tmp, sizeof(double) * h);
+    h = h << 1;
+  }
+  free(tmp);
+}
+
+void jwo_fwt2d_forward(const double* x, int rows, int cols, int lvlM, int lvlN, const double* sD,
+                       const double* wD, int M, int tw, double* y) {
+  int mx = rows > cols ? rows : cols;
+  double* a = (double*)malloc(sizeof(double) * mx);
+  double* b = (double*)malloc(sizeof(double) * mx);
+  for (int i = 0; i < rows; i++) jwo_fwt_forward(x + (long)i * cols, cols, lvlN, sD, wD, M, tw,
+                                                  y + (long)i * cols);
+  for (int j = 0; j < cols; j++) {
+    for (int i = 0; i < rows; i++) a[i] = y[(long)i * cols + j];
+    jwo_fwt_forward(a, rows, lvlM, sD, wD, M, tw, b);
+    for (int i = 0; i < rows; i++) y[(long)i * cols + j] = b[i];
+  }
+  free(a); free(b);
+}
+
+void jwo_fwt2d_reverse(const double* y, int rows, int cols, int lvlM, int lvlN, const double* sR,
+                       const double* wR, int M, int tw, int kind, double* x) {
+  int mx = rows > cols ? rows : cols;
+  double* a = (double*)malloc(sizeof(double) * mx);
+  double* b = (double*)malloc(sizeof(double) * mx);
+  for (int j = 0; j < cols; j++) {
+    for (int i = 0; i < rows; i++) a[i] = y[(long)i * cols + j];
+    jwo_fwt_reverse(a, rows, lvlM, sR, wR, M, tw, kind, b);
+    for (int i = 0; i < rows; i++) x[(long)i * cols + j] = b[i];
+  }
+  for (int i = 0; i < rows; i++) {
+    memcpy(a, x + (long)i * cols, sizeof(double) * cols);
+    jwo_fwt_reverse(a, cols, lvlN, sR, wR, M, tw, kind, x + (long)i * cols);
+  }
+  free(a); free(b);
+}
+
+/* ------------------------------------------------------------------------ */
+/* CWT FFT path: ContinuousWaveletTransform.transformFFT :183-229, padSignal :269-306, */
+/* createFrequencyAxis :450-459, ContinuousWavelet.fourierTransform :122-141,          */
+/* MorletWavelet.fourierTransform :114-124, MexicanHatWavelet :65-119.                */
+/* ------------------------------------------------------------------------ */
+double jwo_cwt_wavelet_ft(int wavelet, const double* params, double omega, double scale) {
+  double w = scale * omega; /* fourierTransform(scale * omega) */
+  double value;
+  if (wavelet == 0) {
+    double fb = params[0], fc = params[1];
+    double f = w / (2.0 * JAVA_PI);
+    double norm = sqrt(2.0 * JAVA_PI * fb);
+    double exponent = -2.0 * JAVA_PI * JAVA_PI * fb * (f - fc) * (f - fc);
+    value = norm * exp(exponent);
+  } else {
+    double sigma = params[0];
+    double nc = 2.0 / (sqrt(3.0 * sigma) * pow(JAVA_PI, 0.25));
+    double ftNorm = nc * sigma * sqrt(2.0 * JAVA_PI);
+    double omega2 = w * w;
+    value = ftNorm * omega2 * exp(-0.5 * sigma * sigma * omega2);
+  }
+  return value * sqrt(scale); /* ft.mul(Math.sqrt(scale)) (real part) */
+}
+
+void jwo_cwt_fft(int wavelet, const double* params, const double* x, long n,
+                 const double* scales, int ns, double fs, int padding, double* out_reim) {
+  long np = 1;
+  if (n > 1) { np = 1; while (np < n) np <<= 1; } /* MathUtils.nextPowerOfTwo */
+  double* X = (double*)calloc(2 * np, sizeof(double));
+  for (long i = 0; i < n; i++) X[2 * i] = x[i];
+  for (long i = n; i < np; i++) {
+    double v = 0.0;
+    if (padding == 1) {
+      long mi = 2 * n - i - 2;
+      if (mi >= 0 && mi < n) v = x[mi];
+    } else if (padding == 2) {
+      v = x[i % n];
+    } else if (padding == 3) {
+      v = x[n - 1];
+    }
+    X[2 * i] = v;
+  }
+  jwo_fft(X, np, 0);
+  double* omega = (double*)malloc(sizeof(double) * np);
+  for (long i = 0; i < np; i++) {
+    omega[i] = 2.0 * JAVA_PI * (double)i * fs / (double)np;
+    if (i > np / 2) omega[i] -= 2.0 * JAVA_PI * fs;
+  }
+  double* P = (double*)malloc(sizeof(double) * 2 * np);
+  for (int s = 0; s < ns; s++) {
+    double scale = scales[s];
+    for (long i = 0; i < np; i++) {
+      double wr = jwo_cwt_wavelet_ft(wavelet, params, omega[i], scale);
+      double wi = 0.0 * sqrt(scale); /* imaginary part of ft.mul(sqrt(a)) */
+      wi = -wi;                      /* conjugate() */
+      double sr = X[2 * i], si = X[2 * i + 1];
+      P[2 * i] = sr * wr - si * wi;
+      P[2 * i + 1] = sr * wi + si * wr;
+    }
+    jwo_fft(P, np, 1);
+    memcpy(out_reim + (long)s * n * 2, P, sizeof(double) * 2 * n);
+  }
+  free(X); free(omega); free(P);
+}
+
+/* ------------------------------------------------------------------------ */
+/* CPU baseline: ForkJoin-equivalent parallel loop over the batch (OpenMP).        */
+/* ------------------------------------------------------------------------ */
+void jwo_modwt_fwdinv_batch(const double* x, long N, int J, const double* g, const double* h,
+                            int L, int B, int use_fft, int threads, double* coeffs, double* xr) {
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+  for (int b = 0; b < B; b++) {
+    double* c = coeffs + (long)b * (J + 1) * N;
+    if (use_fft) {
+      jwo_modwt_forward_fft(x + (long)b * N, N, J, g, h, L, c);
+      jwo_modwt_inverse_fft(c, N, J, g, h, L, xr + (long)b * N);
+    } else {
+      jwo_modwt_forward_direct(x + (long)b * N, N, J, g, h, L, c);
+      jwo_modwt_inverse_direct(c, N, J, g, h, L, xr + (long)b * N);
+    }
+  }
+}

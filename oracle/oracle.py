@@ -1,0 +1,159 @@
+"""TEST INFRASTRUCTURE ONLY: numpy front-end of the C restatement (oracle/liboracle.so).
+
+This is the parity checker for the HIP engine and the "port" CPU baseline of bench.py.
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import it; the
+product package (jwave-pro_amd/jwave) never does.  Reference citations are in
+oracle/jwave_oracle.c.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        _lib = ctypes.CDLL(LIB)
+        _lib.jwo_random_next_double.restype = ctypes.c_double
+        _lib.jwo_cwt_wavelet_ft.restype = ctypes.c_double
+        _lib.jwo_modwt_upsample.restype = ctypes.c_long
+    return _lib
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def _f64(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+
+
+def fill_uniform(n, seed, start=0):
+    """java.util.Random(seed).nextDouble()*2-1, elements [start, start+n)."""
+    out = np.empty(n)
+    if start == 0:
+        lib().jwo_fill_uniform(_p(out), ctypes.c_long(n), ctypes.c_int64(seed))
+    else:
+        lib().jwo_fill_uniform_range(_p(out), ctypes.c_long(start), ctypes.c_long(n),
+                                     ctypes.c_int64(seed))
+    return out
+
+
+def java_random_doubles(seed, n):
+    class R(ctypes.Structure):
+        _fields_ = [("seed", ctypes.c_uint64)]
+    r = R()
+    lib().jwo_random_init(ctypes.byref(r), ctypes.c_int64(seed))
+    return [lib().jwo_random_next_double(ctypes.byref(r)) for _ in range(n)]
+
+
+def modwt_filters(scal, wav):
+    scal, wav = _f64(scal), _f64(wav)
+    L = scal.shape[0]
+    g, h = np.empty(L), np.empty(L)
+    lib().jwo_modwt_filters(_p(scal), _p(wav), L, _p(g), _p(h))
+    return g, h
+
+
+def modwt_forward(x, J, g, h, method="direct"):
+    x, g, h = _f64(x), _f64(g), _f64(h)
+    N = x.shape[0]
+    out = np.empty((J + 1, N))
+    fn = {"fft": lib().jwo_modwt_forward_fft, "direct": lib().jwo_modwt_forward_direct,
+          "direct_nz": lib().jwo_modwt_forward_direct_nz}[method]
+    fn(_p(x), ctypes.c_long(N), J, _p(g), _p(h), g.shape[0], _p(out))
+    return out
+
+
+def modwt_inverse(coeffs, g, h, method="direct"):
+    c, g, h = _f64(coeffs), _f64(g), _f64(h)
+    J = c.shape[0] - 1
+    N = c.shape[1]
+    out = np.empty(N)
+    fn = {"fft": lib().jwo_modwt_inverse_fft, "direct": lib().jwo_modwt_inverse_direct,
+          "direct_nz": lib().jwo_modwt_inverse_direct_nz}[method]
+    fn(_p(c), ctypes.c_long(N), J, _p(g), _p(h), g.shape[0], _p(out))
+    return out
+
+
+def auto_uses_fft(N, M, threshold=4096):
+    return bool(lib().jwo_modwt_auto_uses_fft(ctypes.c_long(N), ctypes.c_long(M), threshold))
+
+
+def fft(x, inverse=False):
+    """FastFourierTransform.forward/reverse on complex input (returns complex ndarray)."""
+    z = np.asarray(x, dtype=np.complex128)
+    buf = np.empty(2 * z.shape[0])
+    buf[0::2], buf[1::2] = z.real, z.imag
+    lib().jwo_fft(_p(buf), ctypes.c_long(z.shape[0]), 1 if inverse else 0)
+    return buf[0::2] + 1j * buf[1::2]
+
+
+def fwt_forward(x, level, wavelet):
+    x = _f64(x)
+    y = np.empty_like(x)
+    sD, wD = _f64(wavelet.getScalingDeComposition()), _f64(wavelet.getWaveletDeComposition())
+    lib().jwo_fwt_forward(_p(x), ctypes.c_long(x.shape[0]), level, _p(sD), _p(wD), sD.shape[0],
+                          wavelet.getTransformWavelength(), _p(y))
+    return y
+
+
+def fwt_reverse(y, level, wavelet):
+    y = _f64(y)
+    x = np.empty_like(y)
+    sR, wR = _f64(wavelet.getScalingReConstruction()), _f64(wavelet.getWaveletReConstruction())
+    lib().jwo_fwt_reverse(_p(y), ctypes.c_long(y.shape[0]), level, _p(sR), _p(wR), sR.shape[0],
+                          wavelet.getTransformWavelength(), getattr(wavelet, "kind", 0), _p(x))
+    return x
+
+
+def fwt2d_forward(x, lvlM, lvlN, wavelet):
+    x = _f64(x)
+    y = np.empty_like(x)
+    sD, wD = _f64(wavelet.getScalingDeComposition()), _f64(wavelet.getWaveletDeComposition())
+    lib().jwo_fwt2d_forward(_p(x), x.shape[0], x.shape[1], lvlM, lvlN, _p(sD), _p(wD),
+                            sD.shape[0], wavelet.getTransformWavelength(), _p(y))
+    return y
+
+
+def fwt2d_reverse(y, lvlM, lvlN, wavelet):
+    y = _f64(y)
+    x = np.empty_like(y)
+    sR, wR = _f64(wavelet.getScalingReConstruction()), _f64(wavelet.getWaveletReConstruction())
+    lib().jwo_fwt2d_reverse(_p(y), y.shape[0], y.shape[1], lvlM, lvlN, _p(sR), _p(wR),
+                            sR.shape[0], wavelet.getTransformWavelength(),
+                            getattr(wavelet, "kind", 0), _p(x))
+    return x
+
+
+def cwt_fft(x, scales, fs=1.0, wavelet="morlet", params=(1.0, 1.0), padding=1):
+    x, sc = _f64(x), _f64(scales)
+    pr = _f64(params)
+    n, ns = x.shape[0], sc.shape[0]
+    out = np.empty((ns, n, 2))
+    lib().jwo_cwt_fft(0 if wavelet == "morlet" else 1, _p(pr), _p(x), ctypes.c_long(n), _p(sc),
+                      ns, ctypes.c_double(fs), padding, _p(out))
+    return out[..., 0] + 1j * out[..., 1]
+
+
+def modwt_fwdinv_batch(x, J, g, h, use_fft=False, threads=0):
+    """CPU-baseline kernel: forward + inverse of every row of x, OpenMP over signals."""
+    x, g, h = _f64(x), _f64(g), _f64(h)
+    B, N = x.shape
+    coeffs = np.empty((B, J + 1, N))
+    xr = np.empty((B, N))
+    lib().jwo_modwt_fwdinv_batch(_p(x), ctypes.c_long(N), J, _p(g), _p(h), g.shape[0], B,
+                                 1 if use_fft else 0, threads, _p(coeffs), _p(xr))
+    return coeffs, xr

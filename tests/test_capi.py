@@ -1,0 +1,143 @@
+"""The C-ABI boundary without a GPU: the library loads, exports every symbol the header
+declares, builds plans bit-identical to the oracle's filter cache, and reproduces the
+reference's validation order, exception classes and messages (all raised before any
+device work).  CPU only.
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle as orc
+from _util import bits_equal
+from conftest import ROOT
+from jwave import MODWTTransform, FastWaveletTransform, Transform, _native
+from jwave.exceptions import IllegalArgumentException, JWaveFailure
+from jwave.transforms import wavelets as W
+
+HEADER = os.path.join(ROOT, "include", "jwave_hip.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(jw_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _native.lib()
+    declared = header_functions()
+    assert declared, "no declarations parsed"
+    assert sorted(_native.EXPORTS) == declared
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert b"gfx950" in lib.jw_version()
+
+
+@pytest.mark.parametrize("wname", W.ORTHONORMAL)
+def test_plan_filters_bit_identical_to_oracle(wname):
+    # MODWTTransform.initializeFilterCache (:452-484) in the C-ABI plan vs the oracle
+    wv = W.by_name(wname)
+    g, h = MODWTTransform(wv).getModwtFilters()
+    og, oh = orc.modwt_filters(wv.getScalingDeComposition(), wv.getWaveletDeComposition())
+    assert bits_equal(g, og) and bits_equal(h, oh)
+
+
+# ---- MODWTTheoreticalLimitTest.java:129-162, MODWTLevelLimitTest.java ----
+def test_forward_level_below_one():
+    m = MODWTTransform(W.Daubechies4())
+    with pytest.raises(IllegalArgumentException, match="at least 1"):
+        m.forwardMODWT(np.ones(8), 0)
+
+
+def test_forward_level_above_13_checked_before_theoretical_limit():
+    m = MODWTTransform(W.Daubechies4())
+    with pytest.raises(IllegalArgumentException) as e:
+        m.forwardMODWT(np.ones(8), 14)
+    assert "maximum supported decomposition level is 13" in str(e.value)
+    assert "theoretical limit" not in str(e.value)
+
+
+@pytest.mark.parametrize("n,limit", [(8, 3), (100, 6), (1023, 9), (1024, 10), (1025, 10)])
+def test_forward_theoretical_limit(n, limit):
+    m = MODWTTransform(W.Haar1())
+    with pytest.raises(IllegalArgumentException) as e:
+        m.forwardMODWT(np.ones(n), limit + 1)
+    msg = str(e.value)
+    assert "exceeds theoretical limit" in msg and str(limit) in msg and str(n) in msg
+
+
+def test_forward_empty_input():
+    # MODWTTransformTest.testEmptyInput: J+1 empty rows
+    c = MODWTTransform(W.Haar1()).forwardMODWT(np.zeros(0), 3)
+    assert len(c) == 4 and all(len(r) == 0 for r in c)
+
+
+def test_inverse_empty_and_single_row():
+    m = MODWTTransform(W.Haar1())
+    assert len(m.inverseMODWT(None)) == 0
+    assert len(m.inverseMODWT([])) == 0
+    assert len(m.inverseMODWT(np.ones((1, 8)))) == 0
+
+
+def test_inverse_level_above_13():
+    m = MODWTTransform(W.Haar1())
+    with pytest.raises(IllegalArgumentException, match="maximum supported decomposition level is 13"):
+        m.inverseMODWT(np.zeros((15, 16)))
+
+
+# ---- MODWT1DInterfaceTest.java:107-136 ----
+def test_flat_interface_errors():
+    m = MODWTTransform(W.Haar1())
+    with pytest.raises(JWaveFailure, match=r"2\^p"):
+        m.forward(np.ones(7), 1)
+    with pytest.raises(JWaveFailure, match="out of range"):
+        m.forward(np.ones(8), 4)
+    with pytest.raises(JWaveFailure, match="does not match|Invalid coefficient array"):
+        m.reverse(np.ones(10), 1)
+
+
+def test_facade_swallows_checked_exceptions(capsys):
+    # Transform.java:81-90: JWaveException -> printed, null returned
+    t = Transform(FastWaveletTransform(W.Haar1()))
+    assert t.forward(np.ones(6)) is None
+    assert "2^p" in capsys.readouterr().out
+
+
+def test_fwt_validation():
+    f = FastWaveletTransform(W.Daubechies4())
+    with pytest.raises(JWaveFailure, match="FastWaveletTransform#forward - given array length is not 2"):
+        f.forward(np.ones(12), 1)
+    with pytest.raises(JWaveFailure, match="given level is out of range"):
+        f.forward(np.ones(8), 4)
+    with pytest.raises(JWaveFailure, match="FastWaveletTransform#reverse - given level is out of range"):
+        f.reverse(np.ones(8), -1)
+    with pytest.raises(JWaveFailure, match="WaveletTransform#forward - given array length"):
+        f.forward(np.ones(6))
+
+
+def test_precompute_filters_limits():
+    m = MODWTTransform(W.Daubechies4())
+    with pytest.raises(IllegalArgumentException, match="precomputeFilters - decomposition level must be at least 1"):
+        m.precomputeFilters(0)
+    with pytest.raises(IllegalArgumentException, match="maximum supported decomposition level is 13"):
+        m.precomputeFilters(14)
+    assert MODWTTransform.getMaxDecompositionLevel() == 13
+
+
+def test_raw_capi_rejects_bad_arguments():
+    lib = _native.lib()
+    plan = ctypes.c_void_p()
+    g = np.ones(8)
+    assert lib.jw_modwt_plan_create(ctypes.byref(plan), ctypes.c_void_p(g.ctypes.data),
+                                    ctypes.c_void_p(g.ctypes.data), 0, 4096, 0) == _native.JW_ERR_ILLEGAL_ARGUMENT
+    assert lib.jw_modwt_plan_create(ctypes.byref(plan), ctypes.c_void_p(g.ctypes.data),
+                                    ctypes.c_void_p(g.ctypes.data), 8, 4096, 0) == _native.JW_OK
+    x = np.ones(16)
+    c = np.empty(16 * 3)
+    st = lib.jw_modwt_forward(plan, ctypes.c_void_p(x.ctypes.data), ctypes.c_void_p(c.ctypes.data),
+                              16, 2, 1, 1, 7, None)
+    assert st == _native.JW_ERR_ILLEGAL_ARGUMENT and "where" in _native.last_error()
+    lib.jw_modwt_plan_destroy(plan)

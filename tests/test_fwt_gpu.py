@@ -1,0 +1,112 @@
+"""FWT parity on the MI355X: the HIP cascade (through the C-ABI) vs the oracle.
+
+JW_ARITH_STRICT must be bit-identical to the JVM sequence of Wavelet.forward / the
+Wavelet.reverse scatter (src/main/java/jwave/transforms/wavelets/Wavelet.java:236-303) for
+every wavelet, length and level; 2-D follows BasicTransform.java:361-474.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import oracle as orc
+from _util import bits_equal, load_vector
+from jwave import FastWaveletTransform, Transform
+from jwave.transforms import wavelets as W
+
+pytestmark = pytest.mark.gpu
+
+CREATE2ARR = (["Haar1"] + [f"Daubechies{k}" for k in range(2, 21)]
+              + [f"Coiflet{k}" for k in range(1, 6)] + [f"Symlet{k}" for k in range(2, 21)])
+
+
+def wavelet(name):
+    return W.Haar1Orthogonal() if name == "Haar1Orthogonal" else W.by_name(name)
+
+
+@pytest.mark.parametrize("wname", CREATE2ARR + ["Haar1Orthogonal", "Legendre1", "Legendre3"])
+def test_fwt_bit_exact_all_wavelets(wname):
+    wv = wavelet(wname)
+    f = FastWaveletTransform(wv)
+    for n, levels in [(2, [1]), (8, [0, 1, 3]), (64, [2, 6]), (1024, [10, 4])]:
+        x = orc.fill_uniform(n, 3 + n)
+        for lvl in levels:
+            y = f.forward(x, lvl)
+            ref = orc.fwt_forward(x, lvl, wv)
+            assert bits_equal(y, ref), (n, lvl)
+            assert bits_equal(f.reverse(ref, lvl), orc.fwt_reverse(ref, lvl, wv)), (n, lvl)
+
+
+@pytest.mark.parametrize("wname", ["Haar1", "Daubechies8", "Symlet8", "Haar1Orthogonal"])
+@pytest.mark.parametrize("n", [4096, 16384])
+def test_fwt_long_signals(wname, n):
+    # n = 4096 runs one workgroup per signal in LDS, 16384 the per-level global path
+    wv = wavelet(wname)
+    f = FastWaveletTransform(wv)
+    x = orc.fill_uniform(n, 17)
+    lvl = int(math.log2(n))
+    ref = orc.fwt_forward(x, lvl, wv)
+    assert bits_equal(f.forward(x, lvl), ref)
+    assert bits_equal(f.reverse(ref, lvl), orc.fwt_reverse(ref, lvl, wv))
+    assert bits_equal(f.forward(x, 3), orc.fwt_forward(x, 3, wv))
+
+
+def test_fwt_batch():
+    wv = W.Daubechies4()
+    f = FastWaveletTransform(wv)
+    xs = np.stack([orc.fill_uniform(1024, b) for b in range(7)])
+    ys = f.forwardBatch(xs, 10)
+    for b in range(7):
+        assert bits_equal(ys[b], orc.fwt_forward(xs[b], 10, wv))
+    xr = f.reverseBatch(ys, 10)
+    for b in range(7):
+        assert bits_equal(xr[b], orc.fwt_reverse(ys[b], 10, wv))
+
+
+@pytest.mark.parametrize("wname", ["Haar1", "Daubechies8"])
+@pytest.mark.parametrize("rows,cols,lvlM,lvlN", [(64, 32, 6, 5), (256, 256, 8, 8), (128, 512, 3, 9)])
+def test_fwt2d_bit_exact(wname, rows, cols, lvlM, lvlN):
+    wv = W.by_name(wname)
+    f = FastWaveletTransform(wv)
+    x = orc.fill_uniform(rows * cols, 11).reshape(rows, cols)
+    ref = orc.fwt2d_forward(x, lvlM, lvlN, wv)
+    assert bits_equal(f.forward(x, lvlM, lvlN), ref)
+    assert bits_equal(f.reverse(ref, lvlM, lvlN), orc.fwt2d_reverse(ref, lvlM, lvlN, wv))
+
+
+def test_fwt2d_batch():
+    wv = W.Daubechies8()
+    f = FastWaveletTransform(wv)
+    xs = np.stack([orc.fill_uniform(64 * 64, 11 + b).reshape(64, 64) for b in range(3)])
+    ys = f.forward2DBatch(xs, 6, 6)
+    for b in range(3):
+        assert bits_equal(ys[b], orc.fwt2d_forward(xs[b], 6, 6, wv))
+    xr = f.reverse2DBatch(ys, 6, 6)
+    for b in range(3):
+        assert np.max(np.abs(xr[b] - xs[b])) < 1e-10
+
+
+@pytest.mark.parametrize("wname", CREATE2ARR)
+def test_decompose_constant(wname):
+    # DecomposeTest.java:40-120 through the facade
+    t = Transform(FastWaveletTransform(W.by_name(wname)))
+    s2 = math.sqrt(2.)
+    m = t.decompose(np.ones(4))
+    assert np.max(np.abs(m - np.array([[1, 1, 1, 1], [s2, s2, 0, 0], [2, 0, 0, 0]]))) < 1e-8
+    assert np.max(np.abs(t.recompose(m, 0) - 1.0)) < 1e-8
+
+
+def test_haar_fixtures_through_gpu():
+    # transforms/CrossValidationTest.java:183-208
+    x = load_vector("haar_simple_input.txt")
+    y = Transform(FastWaveletTransform(W.Haar1())).forward(x, 1)
+    assert np.max(np.abs(y[:4] - load_vector("haar_level1_approx_manual.txt"))) < 1e-10
+    assert np.max(np.abs(y[4:] - load_vector("haar_level1_detail_manual.txt"))) < 1e-10
+
+
+def test_haar_orthogonal_integer_exact():
+    wv = W.Haar1Orthogonal()
+    f = FastWaveletTransform(wv)
+    x = np.arange(-512.0, 512.0)
+    y = f.forward(x, 10)
+    assert np.all(y == np.round(y)) and bits_equal(f.reverse(y, 10), x)
