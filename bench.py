@@ -160,7 +160,7 @@ def main():
         # forward: read x (8 B) + write J+1 rows (8(J+1) B) per sample; inverse the mirror.
         bytes_per_sample = 8 * (1 + (J + 1))
         per_launch = bytes_per_sample * B * n
-        name, ms = ("modwt_inv_fused", inv_ms) if inv_ms >= fwd_ms else ("modwt_fwd_fused", fwd_ms)
+        name, ms = ("modwt_inv_fast", inv_ms) if inv_ms >= fwd_ms else ("modwt_fwd_fast", fwd_ms)
         achieved = per_launch / (ms * 1e-3) / 1e9
         traffic = None
         if os.path.exists(TRAFFIC_FILE):

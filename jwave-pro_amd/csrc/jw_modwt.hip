@@ -20,7 +20,11 @@
 // right).  A segment starts with a warm-up of ceil(H/C) chunks, H = (L-1)(2^J - 1), whose
 // outputs are not stored.  Positions are taken modulo N, so any N >= 1 (multi-wrap
 // filters included) follows the reference's floorMod semantics.
+#include <cstdlib>
+#include <cstring>
+
 #include "jw_internal.hpp"
+#include "jw_modwt_fast.hpp"
 
 namespace jw {
 namespace {
@@ -409,11 +413,47 @@ Taps make_taps(const ModwtPlan& p) {
   return t;
 }
 
+// JW_MODWT_KERNEL=generic forces the runtime-J kernels (A/B and parity testing).
+bool fast_enabled() {
+  const char* e = std::getenv("JW_MODWT_KERNEL");
+  return !(e && std::strcmp(e, "generic") == 0);
+}
+
+int try_fast_forward(int L, const Taps& t, bool fma, const double* x, double* c, long N, int J,
+                     int B, hipStream_t s) {
+  if (!fast_enabled()) return fast::kNotHandled;
+  switch (L) {
+#define JW_CASE(LL) \
+  case LL:          \
+    return fast::forward<LL>(t, fma, x, c, N, J, B, s);
+    JW_FAST_LENGTHS(JW_CASE)
+#undef JW_CASE
+    default:
+      return fast::kNotHandled;
+  }
+}
+
+int try_fast_inverse(int L, const Taps& t, bool fma, const double* c, double* x, long N, int J,
+                     int B, hipStream_t s) {
+  if (!fast_enabled()) return fast::kNotHandled;
+  switch (L) {
+#define JW_CASE(LL) \
+  case LL:          \
+    return fast::inverse<LL>(t, fma, c, x, N, J, B, s);
+    JW_FAST_LENGTHS(JW_CASE)
+#undef JW_CASE
+    default:
+      return fast::kNotHandled;
+  }
+}
+
 template <int L, bool FMA>
 int forward_impl(const ModwtPlan& p, const double* x, double* coeffs, long N, int J, int batch,
                  hipStream_t s) {
   const Taps t = make_taps<L>(p);
   const long rstride = (long)(J + 1) * N;
+  if (int st = try_fast_forward(L, t, FMA, x, coeffs, N, J, batch, s); st != fast::kNotHandled)
+    return st;
   if (fused_ok(L, J, false)) {
     const size_t lds = fused_lds_bytes(L, J, false);
     const long H = (long)(L - 1) * ((1L << J) - 1);
@@ -461,6 +501,8 @@ int inverse_impl(const ModwtPlan& p, const double* coeffs, double* x, long N, in
                  hipStream_t s) {
   const Taps t = make_taps<L>(p);
   const long rstride = (long)(J + 1) * N;
+  if (int st = try_fast_inverse(L, t, FMA, coeffs, x, N, J, batch, s); st != fast::kNotHandled)
+    return st;
   if (fused_ok(L, J, true)) {
     const size_t lds = fused_lds_bytes(L, J, true);
     const long H = (long)(L - 1) * ((1L << J) - 1);

@@ -1,0 +1,444 @@
+// jw_modwt_fast.hpp -- the steady-state MODWT kernels (filter length L and level count J
+// compile-time).  Same arithmetic, tap order and results as the generic kernels in
+// jw_modwt.hip (and as MODWTTransform.java:256-375 DIRECT); see that file for the reference
+// mapping and DESIGN.md "MODWT kernels" for the design.
+//
+// What makes these the fast path on gfx950:
+//  * every step is straight-line code with a fixed number of vector-memory instructions, so
+//    the compiler waits for a prefetched chunk with a counted s_waitcnt vmcnt(N) instead of
+//    draining the step's coefficient stores (vmcnt counts loads and stores in issue order);
+//  * inputs are prefetched two steps ahead into two register sets (no register moves);
+//  * stores are raw buffer stores whose offset is pushed out of range for samples outside the
+//    workgroup's segment -- the hardware range check drops them, no branch;
+//  * lane-consecutive LDS addressing (bank-conflict free) with immediate offsets (the
+//    dilation is compile-time per level);
+//  * the inverse keeps V_j and W_j interleaved as (V, W) pairs in LDS, so one ds_read_b128
+//    feeds both adjoint sums of a tap and every coefficient is read from HBM once.
+#pragma once
+#include <cstdlib>
+#include <type_traits>
+
+#include "jw_internal.hpp"
+
+namespace jw {
+namespace fast {
+
+constexpr int kC = 512;           // samples per level per step (both directions)
+constexpr int kOOB = 0x7ffff000;  // byte offset beyond any row (N < 2^27): store dropped
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef double d2 __attribute__((ext_vector_type(2)));
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const double* p, long n) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, (int)(n * 8), 0x00020000);
+}
+__device__ __forceinline__ double bload(rsrc_t r, int off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+__device__ __forceinline__ void bstore(rsrc_t r, int off, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, 0);
+}
+
+template <bool FMA>
+__device__ __forceinline__ double madd(double acc, double f, double v) {
+  if constexpr (FMA) {
+    return __builtin_fma(f, v, acc);
+  } else {
+    return acc + f * v;  // -ffp-contract=off: Java's rounded product + rounded sum
+  }
+}
+
+template <int L, int J>
+struct Geo {
+  static constexpr int H = (L - 1) * ((1 << J) - 1);  // total history samples
+  static constexpr int hist(int j) { return (L - 1) << (j - 1); }
+  static constexpr int hoff(int j) { return (L - 1) * ((1 << (j - 1)) - 1); }  // flat history offset
+  // forward: B_{j-1} = [hist_j | C] holds V_{j-1}
+  static constexpr int fwd_off(int j) { return hoff(j) + (j - 1) * kC; }
+  static constexpr int fwd_total = H + J * kC;  // doubles
+  // inverse: VW_j = [C | hist_j] of (V_j, W_j) pairs
+  static constexpr int inv_off(int j) { return hoff(j) + (j - 1) * kC; }  // in pairs
+  static constexpr int inv_total = 2 * (H + J * kC);                       // doubles
+};
+
+// Flat history index e in [0, H) -> level j (1-based).
+template <int L>
+__device__ __forceinline__ int level_of(int e) {
+  const unsigned q = (unsigned)e / (unsigned)(L - 1) + 1u;
+  return 32 - __builtin_clz(q);
+}
+
+// ---------------------------------------------------------------------------------------
+// Forward: left -> right.  Thread t owns samples t + r*NT (r < R = C/NT) of every level.
+// ---------------------------------------------------------------------------------------
+template <int L, int J, bool FMA, int NT, class Fetch>
+__device__ __forceinline__ void fwd_step(double* lds, double (&cur)[kC / NT], Fetch&& fetch,
+                                         long a, long P, long seg_end,
+                                         const rsrc_t (&rw)[J + 1], const Taps& taps) {
+  using G = Geo<L, J>;
+  constexpr int R = kC / NT;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int r = 0; r < R; ++r) lds[G::fwd_off(1) + G::hist(1) + tid + r * NT] = cur[r];
+  fetch(cur);  // the chunk two steps ahead: in flight behind this step and the next
+  __syncthreads();
+#pragma unroll
+  for (int j = 1; j <= J; ++j) {
+    const int d = 1 << (j - 1);
+    const double* src = lds + G::fwd_off(j) + G::hist(j);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int i = tid + r * NT;
+      double w = 0.0, v = 0.0;
+#pragma unroll
+      for (int m = 0; m < L; ++m) {
+        const double xv = src[i - m * d];
+        w = madd<FMA>(w, taps.b[m], xv);
+        v = madd<FMA>(v, taps.a[m], xv);
+      }
+      const long pos = a + i;
+      const int off = (pos >= P && pos < seg_end) ? (int)(pos * 8) : kOOB;
+      bstore(rw[j - 1], off, w);
+      if (j < J) {
+        lds[G::fwd_off(j + 1) + G::hist(j + 1) + i] = v;
+      } else {
+        bstore(rw[J], off, v);
+      }
+    }
+    __syncthreads();
+  }
+  // History shift B_{j-1}[C .. C+hist_j) -> [0 .. hist_j): flat e -> src e + j*C, dst e + (j-1)*C.
+  constexpr int kPer = (G::H + NT - 1) / NT;
+  if constexpr (kPer > 0) {
+    double hv[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const int e = tid + r * NT;
+      if (e < G::H) hv[r] = lds[e + level_of<L>(e) * kC];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const int e = tid + r * NT;
+      if (e < G::H) lds[e + (level_of<L>(e) - 1) * kC] = hv[r];
+    }
+  }
+}
+
+template <int L, int J, bool FMA, int NT>
+__global__ __launch_bounds__(NT) void modwt_fwd_fast(const double* __restrict__ x,
+                                                     double* __restrict__ coeffs, long N,
+                                                     long seg_len, long warm, long npairs,
+                                                     Taps taps) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  using G = Geo<L, J>;
+  constexpr int R = kC / NT;
+  const int tid = threadIdx.x;
+  const long P = (long)blockIdx.x * seg_len;
+  const long seg_end = min(P + seg_len, N);
+  const double* xs = x + (long)blockIdx.y * N;
+  double* cs = coeffs + (long)blockIdx.y * (long)(J + 1) * N;
+  const rsrc_t rx = make_rsrc(xs, N);
+  rsrc_t rw[J + 1];
+#pragma unroll
+  for (int j = 0; j <= J; ++j) rw[j] = make_rsrc(cs + (long)j * N, N);
+  for (int i = tid; i < G::fwd_total; i += NT) lds[i] = 0.0;
+
+  long a = P - warm;
+  long lb = a % N;  // load cursor: stream position of the next chunk to fetch, mod N
+  if (lb < 0) lb += N;
+  auto fetch = [&](double (&dst)[R]) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      long p = lb + tid + r * NT;
+      p = p >= N ? p - N : p;
+      dst[r] = bload(rx, (int)(p * 8));
+    }
+    lb += kC;
+    if (lb >= N) lb -= N;
+  };
+  double A[R], B[R];
+  fetch(A);
+  __builtin_amdgcn_sched_barrier(0);  // keep A's loads strictly older than B's (counted waits)
+  fetch(B);
+  __builtin_amdgcn_sched_barrier(0);
+  // Range-dropped dummy stores give the loop entry the same vector-memory queue depth as the
+  // loop back-edge (two steps of stores + one fetch behind A), so the compiler's merged wait
+  // at the first step is the steady-state counted vmcnt, not a near-drain.
+#pragma unroll
+  for (int i = 0; i < 2 * R * (J + 1); ++i) bstore(rx, kOOB - 8 * i, 0.0);  // distinct: not merged
+  __syncthreads();
+  for (long k = 0; k < npairs; ++k) {
+    fwd_step<L, J, FMA, NT>(lds, A, fetch, a, P, seg_end, rw, taps);
+    a += kC;
+    fwd_step<L, J, FMA, NT>(lds, B, fetch, a, P, seg_end, rw, taps);
+    a += kC;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Inverse: right -> left.  VW_j holds (V_j, W_j) pairs at positions [a, a + C + hist_j);
+// thread t owns samples t + r*NT.  cur[(J+1)*r + (j-1)] = W_j, cur[(J+1)*r + J] = V_J.
+// ---------------------------------------------------------------------------------------
+template <int L, int J, bool FMA, int NT, class Fetch>
+__device__ __forceinline__ void inv_step(d2* vw, double (&cur)[(kC / NT) * (J + 1)],
+                                         Fetch&& fetch, long a, long P, long seg_end,
+                                         const rsrc_t& rx, const Taps& taps) {
+  using G = Geo<L, J>;
+  constexpr int R = kC / NT;
+  const int t = threadIdx.x;
+  double* lds = (double*)vw;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int i = t + r * NT;
+    lds[2 * (G::inv_off(J) + i)] = cur[(J + 1) * r + J];
+#pragma unroll
+    for (int j = 1; j <= J; ++j) lds[2 * (G::inv_off(j) + i) + 1] = cur[(J + 1) * r + j - 1];
+  }
+  fetch(cur);  // the chunk two steps ahead
+  __syncthreads();
+#pragma unroll
+  for (int j = J; j >= 1; --j) {
+    const int d = 1 << (j - 1);
+    const d2* src = vw + G::inv_off(j);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int i = t + r * NT;
+      double ap = 0.0, dp = 0.0;
+#pragma unroll
+      for (int m = 0; m < L; ++m) {
+        const d2 p = src[i + m * d];
+        ap = madd<FMA>(ap, taps.a[m], p.x);
+        dp = madd<FMA>(dp, taps.b[m], p.y);
+      }
+      const double v = ap + dp;  // inverseMODWT :366-369, vFromApprox + vFromDetail
+      if (j > 1) {
+        lds[2 * (G::inv_off(j - 1) + i)] = v;
+      } else {
+        const long pos = a + i;
+        bstore(rx, (pos >= P && pos < seg_end) ? (int)(pos * 8) : kOOB, v);
+      }
+    }
+    __syncthreads();
+  }
+  // History shift of every VW_j: [0 .. hist_j) -> [C .. C + hist_j) (flat e over H pairs:
+  // src e + (j-1)*C, dst e + j*C).
+  constexpr int kPer = (G::H + NT - 1) / NT;
+  if constexpr (kPer > 0) {
+    d2 hv[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const int e = t + r * NT;
+      if (e < G::H) hv[r] = vw[e + (level_of<L>(e) - 1) * kC];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const int e = t + r * NT;
+      if (e < G::H) vw[e + level_of<L>(e) * kC] = hv[r];
+    }
+  }
+}
+
+template <int L, int J, bool FMA, int NT>
+__global__ __launch_bounds__(NT) void modwt_inv_fast(const double* __restrict__ coeffs,
+                                                     double* __restrict__ x, long N,
+                                                     long seg_len, long a_start, long npairs,
+                                                     Taps taps) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  using G = Geo<L, J>;
+  constexpr int R = kC / NT;
+  const int t = threadIdx.x;
+  const long P = (long)blockIdx.x * seg_len;
+  const long seg_end = min(P + seg_len, N);
+  const double* cs = coeffs + (long)blockIdx.y * (long)(J + 1) * N;
+  const rsrc_t rx = make_rsrc(x + (long)blockIdx.y * N, N);
+  rsrc_t rc[J + 1];
+#pragma unroll
+  for (int j = 0; j <= J; ++j) rc[j] = make_rsrc(cs + (long)j * N, N);
+  for (int i = t; i < G::inv_total; i += NT) lds[i] = 0.0;
+
+  long a = P + a_start;  // rightmost chunk start (segment end + warm-up, chunk aligned)
+  long lb = a % N;
+  auto fetch = [&](double (&dst)[R * (J + 1)]) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      long p = lb + t + r * NT;
+      p = p >= N ? p - N : p;
+      const int off = (int)(p * 8);
+#pragma unroll
+      for (int j = 0; j <= J; ++j) dst[(J + 1) * r + j] = bload(rc[j], off);
+    }
+    lb -= kC;
+    if (lb < 0) lb += N;
+  };
+  double A[R * (J + 1)], B[R * (J + 1)];
+  fetch(A);
+  __builtin_amdgcn_sched_barrier(0);  // keep A's loads strictly older than B's (counted waits)
+  fetch(B);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < 2 * R; ++i) bstore(rx, kOOB - 8 * i, 0.0);  // queue-depth padding
+  __syncthreads();
+  for (long k = 0; k < npairs; ++k) {
+    inv_step<L, J, FMA, NT>((d2*)lds, A, fetch, a, P, seg_end, rx, taps);
+    a -= kC;
+    inv_step<L, J, FMA, NT>((d2*)lds, B, fetch, a, P, seg_end, rx, taps);
+    a -= kC;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Host launchers (instantiated per filter length in jw_modwt_fast_l*.hip)
+// ---------------------------------------------------------------------------------------
+template <int L, int J>
+constexpr bool fwd_ok() {
+  return (size_t)Geo<L, J>::fwd_total * 8 <= 80 * 1024 && Geo<L, J>::H <= 16 * 256;
+}
+template <int L, int J>
+constexpr bool inv_ok() {
+  return (size_t)Geo<L, J>::inv_total * 8 <= 160 * 1024 && Geo<L, J>::H <= 16 * 256;
+}
+
+// Threads per workgroup (C = 512 samples per step either way): env JW_FWD_NT / JW_INV_NT
+// (256 or 512) for A/B runs; defaults are the measured best.
+inline int pick_nt(const char* env, int dflt) {
+  const char* e = std::getenv(env);
+  if (e && e[0] == '2') return 256;
+  if (e && e[0] == '5') return 512;
+  return dflt;
+}
+
+// Segment of a signal per workgroup: whole chunks, at least 8x the warm-up, and enough
+// segments that the grid holds several waves of workgroups.
+inline long pick_seg(long N, int batch, long warm) {
+  const long nchunks = (N + kC - 1) / kC;
+  long min_chunks = (8 * warm) / kC;
+  if (min_chunks < 1) min_chunks = 1;
+  long seg_chunks = nchunks;
+  while (seg_chunks > min_chunks && (long)batch * ((nchunks + seg_chunks - 1) / seg_chunks) < 8192)
+    seg_chunks = (seg_chunks + 1) / 2;
+  if (seg_chunks < min_chunks) seg_chunks = min_chunks < nchunks ? min_chunks : nchunks;
+  return seg_chunks * kC;
+}
+
+template <class K>
+int launch(K kern, size_t lds, long nseg, int batch, int nt, hipStream_t s, const double* in,
+           long in_stride, double* out, long out_stride, long N, long seg, long p4, long npairs,
+           const Taps& t) {
+  JW_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)lds));
+  for (int b0 = 0; b0 < batch; b0 += 65535) {
+    const int nb = batch - b0 < 65535 ? batch - b0 : 65535;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nseg, (unsigned)nb), dim3(nt), lds, s,
+                       in + (long)b0 * in_stride, out + (long)b0 * out_stride, N, seg, p4, npairs,
+                       t);
+  }
+  JW_HIP_TRY(hipGetLastError());
+  return JW_OK;
+}
+
+template <int L, int J, bool FMA>
+int launch_fwd(const Taps& t, const double* x, double* c, long N, int batch, hipStream_t s) {
+  using G = Geo<L, J>;
+  const long warm = ((long)(G::H + kC - 1) / kC) * kC;
+  const long seg = pick_seg(N, batch, warm);
+  const long nseg = (N + seg - 1) / seg;
+  const long npairs = ((seg + warm) / kC + 1) / 2;  // an odd extra step runs right of the segment
+  const size_t lds = (size_t)G::fwd_total * sizeof(double);
+  const long cs = (long)(J + 1) * N;
+  if (pick_nt("JW_FWD_NT", 256) == 512)
+    return launch(modwt_fwd_fast<L, J, FMA, 512>, lds, nseg, batch, 512, s, x, N, c, cs, N, seg,
+                  warm, npairs, t);
+  return launch(modwt_fwd_fast<L, J, FMA, 256>, lds, nseg, batch, 256, s, x, N, c, cs, N, seg,
+                warm, npairs, t);
+}
+
+template <int L, int J, bool FMA>
+int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hipStream_t s) {
+  using G = Geo<L, J>;
+  const long warm = ((long)(G::H + kC - 1) / kC) * kC;
+  const long seg = pick_seg(N, batch, warm);
+  const long nseg = (N + seg - 1) / seg;
+  const long steps = seg / kC + warm / kC;
+  const long npairs = (steps + 1) / 2;
+  const long a_start = (steps - 1) * kC;  // an odd extra step runs left of the segment
+  const size_t lds = (size_t)G::inv_total * sizeof(double);
+  const long cs = (long)(J + 1) * N;
+  if (pick_nt("JW_INV_NT", 512) == 512)
+    return launch(modwt_inv_fast<L, J, FMA, 512>, lds, nseg, batch, 512, s, c, cs, x, N, N, seg,
+                  a_start, npairs, t);
+  return launch(modwt_inv_fast<L, J, FMA, 256>, lds, nseg, batch, 256, s, c, cs, x, N, N, seg,
+                a_start, npairs, t);
+}
+
+// Returned when (L, J, N) has no fast kernel (the caller falls back to the generic ones).
+constexpr int kNotHandled = -100;
+
+template <int L>
+int forward(const Taps& t, bool fma, const double* x, double* c, long N, int J, int batch,
+            hipStream_t s) {
+  if (N < kC || N >= (1L << 27)) return kNotHandled;
+  int st = kNotHandled;
+  auto one = [&](auto jc) {
+    constexpr int JJ = decltype(jc)::value;
+    if constexpr (fwd_ok<L, JJ>()) {
+      st = fma ? launch_fwd<L, JJ, true>(t, x, c, N, batch, s)
+               : launch_fwd<L, JJ, false>(t, x, c, N, batch, s);
+    }
+  };
+  switch (J) {
+#define JW_J(JJ)                            \
+  case JJ:                                  \
+    one(std::integral_constant<int, JJ>{}); \
+    break;
+    JW_J(1) JW_J(2) JW_J(3) JW_J(4) JW_J(5) JW_J(6) JW_J(7) JW_J(8) JW_J(9) JW_J(10)
+#undef JW_J
+    default:
+      break;
+  }
+  return st;
+}
+
+template <int L>
+int inverse(const Taps& t, bool fma, const double* c, double* x, long N, int J, int batch,
+            hipStream_t s) {
+  if (N < kC || N >= (1L << 27)) return kNotHandled;
+  int st = kNotHandled;
+  auto one = [&](auto jc) {
+    constexpr int JJ = decltype(jc)::value;
+    if constexpr (inv_ok<L, JJ>()) {
+      st = fma ? launch_inv<L, JJ, true>(t, c, x, N, batch, s)
+               : launch_inv<L, JJ, false>(t, c, x, N, batch, s);
+    }
+  };
+  switch (J) {
+#define JW_J(JJ)                            \
+  case JJ:                                  \
+    one(std::integral_constant<int, JJ>{}); \
+    break;
+    JW_J(1) JW_J(2) JW_J(3) JW_J(4) JW_J(5) JW_J(6) JW_J(7) JW_J(8) JW_J(9) JW_J(10)
+#undef JW_J
+    default:
+      break;
+  }
+  return st;
+}
+
+#define JW_FAST_EXTERN(LL)                                                                     \
+  extern template int forward<LL>(const Taps&, bool, const double*, double*, long, int, int,   \
+                                  hipStream_t);                                                \
+  extern template int inverse<LL>(const Taps&, bool, const double*, double*, long, int, int,   \
+                                  hipStream_t);
+#define JW_FAST_INSTANTIATE(LL)                                                                \
+  template int forward<LL>(const Taps&, bool, const double*, double*, long, int, int,          \
+                           hipStream_t);                                                       \
+  template int inverse<LL>(const Taps&, bool, const double*, double*, long, int, int,          \
+                           hipStream_t);
+#define JW_FAST_LENGTHS(X) X(2) X(4) X(6) X(8) X(12) X(16) X(20)
+
+JW_FAST_LENGTHS(JW_FAST_EXTERN)
+
+}  // namespace fast
+}  // namespace jw

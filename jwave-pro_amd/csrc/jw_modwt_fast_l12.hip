@@ -1,0 +1,8 @@
+// Fast MODWT kernels for filter length 12 (see jw_modwt_fast.hpp).
+#include "jw_modwt_fast.hpp"
+
+namespace jw {
+namespace fast {
+JW_FAST_INSTANTIATE(12)
+}  // namespace fast
+}  // namespace jw

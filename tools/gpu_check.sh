@@ -1,0 +1,21 @@
+#!/bin/bash
+# One GPU session: parity tests, then (only if no crash) the bench and a rocprofv3 kernel trace.
+# Every GPU step has its own time limit; a crash/timeout ends the script.
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$R" || exit 2
+mkdir -p gpurun_out
+TAG="${1:-r01}"
+timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x > gpurun_out/pytest_gpu_$TAG.log 2>&1
+rc=$?
+echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu_$TAG.log
+if [ $rc -gt 1 ]; then exit $rc; fi
+timeout -k 10 600 python bench.py --steps 10 --warmup 2 > gpurun_out/bench_$TAG.log 2>&1
+rc=$?
+echo "bench rc=$rc"; tail -3 gpurun_out/bench_$TAG.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$TAG" -o run --output-format csv \
+  -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-check > "$R/gpurun_out/prof_$TAG.log" 2>&1
+rc=$?
+echo "rocprof rc=$rc"; tail -2 "$R/gpurun_out/prof_$TAG.log"
+exit $rc

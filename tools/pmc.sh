@@ -1,0 +1,19 @@
+#!/bin/bash
+# rocprofv3 PMC passes over a short bench run (counters in separate passes; --kernel-trace only,
+# never combined with sys/runtime traces).  Usage: tools/pmc.sh TAG [bench args...]
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+TAG="$1"; shift
+mkdir -p "$R/gpurun_out/pmc_$TAG"
+cd /tmp && export TMPDIR=/tmp
+i=0
+for ctrs in "FETCH_SIZE" "WRITE_SIZE" \
+            "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS" \
+            "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  timeout -k 10 400 rocprofv3 --kernel-trace --pmc $ctrs -d "$R/gpurun_out/pmc_$TAG/p$i" -o run \
+      --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline --no-check "$@" \
+      > "$R/gpurun_out/pmc_$TAG/p$i.log" 2>&1
+  rc=$?
+  echo "pass $i ($ctrs) rc=$rc"
+  if [ $rc -ne 0 ]; then tail -5 "$R/gpurun_out/pmc_$TAG/p$i.log"; exit $rc; fi
+done
