@@ -57,9 +57,14 @@ struct Geo {
   // forward: B_{j-1} = [hist_j | C] holds V_{j-1}
   static constexpr int fwd_off(int j) { return hoff(j) + (j - 1) * kC; }
   static constexpr int fwd_total = H + J * kC;  // doubles
-  // inverse: VW_j = [C | hist_j] of (V_j, W_j) pairs
-  static constexpr int inv_off(int j) { return hoff(j) + (j - 1) * kC; }  // in pairs
-  static constexpr int inv_total = 2 * (H + J * kC);                       // doubles
+};
+
+// Inverse layout: VW_j = [C | hist_j] of (V_j, W_j) pairs, C samples per step.
+template <int L, int J, int C>
+struct GeoI {
+  static constexpr int H = Geo<L, J>::H;
+  static constexpr int inv_off(int j) { return Geo<L, J>::hoff(j) + (j - 1) * C; }  // pairs
+  static constexpr int inv_total = 2 * (H + J * C);                                  // doubles
 };
 
 // Flat history index e in [0, H) -> level j (1-based).
@@ -181,20 +186,22 @@ __global__ __launch_bounds__(NT) void modwt_fwd_fast(const double* __restrict__ 
 // Inverse: right -> left.  VW_j holds (V_j, W_j) pairs at positions [a, a + C + hist_j);
 // thread t owns samples t + r*NT.  cur[(J+1)*r + (j-1)] = W_j, cur[(J+1)*r + J] = V_J.
 // ---------------------------------------------------------------------------------------
-template <int L, int J, bool FMA, int NT, class Fetch>
-__device__ __forceinline__ void inv_step(d2* vw, double (&cur)[(kC / NT) * (J + 1)],
+template <int L, int J, bool FMA, int C, int NT, class Fetch>
+__device__ __forceinline__ void inv_step(d2* vw, double (&cur)[(C / NT) * (J + 1)],
                                          Fetch&& fetch, long a, long P, long seg_end,
                                          const rsrc_t& rx, const Taps& taps) {
-  using G = Geo<L, J>;
-  constexpr int R = kC / NT;
+  using G = GeoI<L, J, C>;
+  constexpr int R = C / NT;
   const int t = threadIdx.x;
-  double* lds = (double*)vw;
+  // W_j samples of this step stay in registers until V_j is known (level j+1), so every
+  // (V_j, W_j) pair reaches LDS as one 16-byte store (8-byte stores at a 16-byte stride
+  // would conflict 2-way).
+  double wj[R][J];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const int i = t + r * NT;
-    lds[2 * (G::inv_off(J) + i)] = cur[(J + 1) * r + J];
+    vw[G::inv_off(J) + t + r * NT] = d2{cur[(J + 1) * r + J], cur[(J + 1) * r + J - 1]};
 #pragma unroll
-    for (int j = 1; j <= J; ++j) lds[2 * (G::inv_off(j) + i) + 1] = cur[(J + 1) * r + j - 1];
+    for (int j = 1; j < J; ++j) wj[r][j] = cur[(J + 1) * r + j - 1];
   }
   fetch(cur);  // the chunk two steps ahead
   __syncthreads();
@@ -214,7 +221,7 @@ __device__ __forceinline__ void inv_step(d2* vw, double (&cur)[(kC / NT) * (J + 
       }
       const double v = ap + dp;  // inverseMODWT :366-369, vFromApprox + vFromDetail
       if (j > 1) {
-        lds[2 * (G::inv_off(j - 1) + i)] = v;
+        vw[G::inv_off(j - 1) + i] = d2{v, wj[r][j - 1]};
       } else {
         const long pos = a + i;
         bstore(rx, (pos >= P && pos < seg_end) ? (int)(pos * 8) : kOOB, v);
@@ -230,25 +237,25 @@ __device__ __forceinline__ void inv_step(d2* vw, double (&cur)[(kC / NT) * (J + 
 #pragma unroll
     for (int r = 0; r < kPer; ++r) {
       const int e = t + r * NT;
-      if (e < G::H) hv[r] = vw[e + (level_of<L>(e) - 1) * kC];
+      if (e < G::H) hv[r] = vw[e + (level_of<L>(e) - 1) * C];
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kPer; ++r) {
       const int e = t + r * NT;
-      if (e < G::H) vw[e + level_of<L>(e) * kC] = hv[r];
+      if (e < G::H) vw[e + level_of<L>(e) * C] = hv[r];
     }
   }
 }
 
-template <int L, int J, bool FMA, int NT>
+template <int L, int J, bool FMA, int C, int NT>
 __global__ __launch_bounds__(NT) void modwt_inv_fast(const double* __restrict__ coeffs,
                                                      double* __restrict__ x, long N,
                                                      long seg_len, long a_start, long npairs,
                                                      Taps taps) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  using G = Geo<L, J>;
-  constexpr int R = kC / NT;
+  using G = GeoI<L, J, C>;
+  constexpr int R = C / NT;
   const int t = threadIdx.x;
   const long P = (long)blockIdx.x * seg_len;
   const long seg_end = min(P + seg_len, N);
@@ -270,7 +277,7 @@ __global__ __launch_bounds__(NT) void modwt_inv_fast(const double* __restrict__ 
 #pragma unroll
       for (int j = 0; j <= J; ++j) dst[(J + 1) * r + j] = bload(rc[j], off);
     }
-    lb -= kC;
+    lb -= C;
     if (lb < 0) lb += N;
   };
   double A[R * (J + 1)], B[R * (J + 1)];
@@ -282,10 +289,10 @@ __global__ __launch_bounds__(NT) void modwt_inv_fast(const double* __restrict__ 
   for (int i = 0; i < 2 * R; ++i) bstore(rx, kOOB - 8 * i, 0.0);  // queue-depth padding
   __syncthreads();
   for (long k = 0; k < npairs; ++k) {
-    inv_step<L, J, FMA, NT>((d2*)lds, A, fetch, a, P, seg_end, rx, taps);
-    a -= kC;
-    inv_step<L, J, FMA, NT>((d2*)lds, B, fetch, a, P, seg_end, rx, taps);
-    a -= kC;
+    inv_step<L, J, FMA, C, NT>((d2*)lds, A, fetch, a, P, seg_end, rx, taps);
+    a -= C;
+    inv_step<L, J, FMA, C, NT>((d2*)lds, B, fetch, a, P, seg_end, rx, taps);
+    a -= C;
   }
 }
 
@@ -296,9 +303,13 @@ template <int L, int J>
 constexpr bool fwd_ok() {
   return (size_t)Geo<L, J>::fwd_total * 8 <= 80 * 1024 && Geo<L, J>::H <= 16 * 256;
 }
+template <int L, int J, int C>
+constexpr bool inv_fits() {
+  return (size_t)GeoI<L, J, C>::inv_total * 8 <= 160 * 1024 && Geo<L, J>::H <= 16 * C;
+}
 template <int L, int J>
 constexpr bool inv_ok() {
-  return (size_t)Geo<L, J>::inv_total * 8 <= 160 * 1024 && Geo<L, J>::H <= 16 * 256;
+  return inv_fits<L, J, 256>();
 }
 
 // Threads per workgroup (C = 512 samples per step either way): env JW_FWD_NT / JW_INV_NT
@@ -312,15 +323,15 @@ inline int pick_nt(const char* env, int dflt) {
 
 // Segment of a signal per workgroup: whole chunks, at least 8x the warm-up, and enough
 // segments that the grid holds several waves of workgroups.
-inline long pick_seg(long N, int batch, long warm) {
-  const long nchunks = (N + kC - 1) / kC;
-  long min_chunks = (8 * warm) / kC;
+inline long pick_seg(long N, int batch, long warm, int C = kC) {
+  const long nchunks = (N + C - 1) / C;
+  long min_chunks = (8 * warm) / C;
   if (min_chunks < 1) min_chunks = 1;
   long seg_chunks = nchunks;
   while (seg_chunks > min_chunks && (long)batch * ((nchunks + seg_chunks - 1) / seg_chunks) < 8192)
     seg_chunks = (seg_chunks + 1) / 2;
   if (seg_chunks < min_chunks) seg_chunks = min_chunks < nchunks ? min_chunks : nchunks;
-  return seg_chunks * kC;
+  return seg_chunks * C;
 }
 
 template <class K>
@@ -355,22 +366,34 @@ int launch_fwd(const Taps& t, const double* x, double* c, long N, int batch, hip
                 warm, npairs, t);
 }
 
-template <int L, int J, bool FMA>
-int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hipStream_t s) {
-  using G = Geo<L, J>;
-  const long warm = ((long)(G::H + kC - 1) / kC) * kC;
-  const long seg = pick_seg(N, batch, warm);
+template <int L, int J, bool FMA, int C>
+int launch_inv_c(const Taps& t, const double* c, double* x, long N, int batch, hipStream_t s) {
+  using G = GeoI<L, J, C>;
+  const long warm = ((long)(G::H + C - 1) / C) * C;
+  const long seg = pick_seg(N, batch, warm, C);
   const long nseg = (N + seg - 1) / seg;
-  const long steps = seg / kC + warm / kC;
+  const long steps = seg / C + warm / C;
   const long npairs = (steps + 1) / 2;
-  const long a_start = (steps - 1) * kC;  // an odd extra step runs left of the segment
+  const long a_start = (steps - 1) * C;  // an odd extra step runs left of the segment
   const size_t lds = (size_t)G::inv_total * sizeof(double);
   const long cs = (long)(J + 1) * N;
-  if (pick_nt("JW_INV_NT", 512) == 512)
-    return launch(modwt_inv_fast<L, J, FMA, 512>, lds, nseg, batch, 512, s, c, cs, x, N, N, seg,
-                  a_start, npairs, t);
-  return launch(modwt_inv_fast<L, J, FMA, 256>, lds, nseg, batch, 256, s, c, cs, x, N, N, seg,
+  return launch(modwt_inv_fast<L, J, FMA, C, C>, lds, nseg, batch, C, s, c, cs, x, N, N, seg,
                 a_start, npairs, t);
+}
+
+// Inverse chunk (= threads per workgroup, one sample each per level): 256 (measured best
+// for db4 J=8: 2 workgroups per CU); env JW_INV_C (256 / 384 / 512) overrides for A/B runs.
+template <int L, int J, bool FMA>
+int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hipStream_t s) {
+  const char* e = std::getenv("JW_INV_C");
+  const int want = e ? std::atoi(e) : 256;
+  if constexpr (inv_fits<L, J, 512>()) {
+    if (want == 512) return launch_inv_c<L, J, FMA, 512>(t, c, x, N, batch, s);
+  }
+  if constexpr (inv_fits<L, J, 384>()) {
+    if (want == 384) return launch_inv_c<L, J, FMA, 384>(t, c, x, N, batch, s);
+  }
+  return launch_inv_c<L, J, FMA, 256>(t, c, x, N, batch, s);
 }
 
 // Returned when (L, J, N) has no fast kernel (the caller falls back to the generic ones).

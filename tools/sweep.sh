@@ -7,14 +7,12 @@ TAG="$1"; shift
 OUT="gpurun_out/sweep_$TAG.log"
 : > "$OUT"
 for arith in fma strict; do
-  for fnt in 256 512; do
-    for int in 256 512; do
-      JW_FWD_NT=$fnt JW_INV_NT=$int timeout -k 10 300 python bench.py --steps 6 --warmup 2 \
-          --arith $arith --no-cpu-baseline --no-check "$@" > /tmp/sw.json 2>/dev/null
-      rc=$?
-      if [ $rc -ne 0 ]; then echo "variant $arith $fnt $int rc=$rc" >> "$OUT"; exit $rc; fi
-      python3 -c "import json,sys; d=json.loads(open('/tmp/sw.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$arith fwd_nt=$fnt inv_nt=$int', d['value'], 'fwd_ms', r['fwd_ms'], 'inv_ms', r['inv_ms'])" >> "$OUT"
-    done
+  for ic in 256 384 512; do
+    JW_INV_C=$ic timeout -k 10 300 python bench.py --steps 6 --warmup 2 \
+        --arith $arith --no-cpu-baseline --no-check "$@" > /tmp/sw.json 2>/dev/null
+    rc=$?
+    if [ $rc -ne 0 ]; then echo "variant $arith $ic rc=$rc" >> "$OUT"; cat "$OUT"; exit $rc; fi
+    python3 -c "import json,sys; d=json.loads(open('/tmp/sw.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$arith inv_c=$ic', d['value'], 'fwd_ms', r['fwd_ms'], 'inv_ms', r['inv_ms'])" >> "$OUT"
   done
 done
 cat "$OUT"
