@@ -75,58 +75,93 @@ __device__ __forceinline__ int level_of(int e) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Forward: left -> right.  Thread t owns samples t + r*NT (r < R = C/NT) of every level.
+// Forward: left -> right.  Thread t owns the adjacent output pair (2t, 2t+1) of every level
+// (C = 2*NT), so every LDS read, LDS write, global load and global store moves 16 bytes per
+// lane.  For d = 2^(j-1) >= 2 the pair's taps are adjacent pairs (x[i-md], x[i+1-md]); for
+// d = 1 the L+1 distinct samples x[i+1-k] come from L/2+1 aligned pairs.  B_{j-1} keeps its
+// chunk 16-byte aligned: logical position p of level j's input lives at cs(j) + p with
+// cs(j) = hoff(j+1) + (j-1)*C + 1 (L even).  Needs N even (pairs never straddle a wrap).
 // ---------------------------------------------------------------------------------------
+template <int L, int J, int C>
+struct GeoF {
+  static constexpr int H = Geo<L, J>::H;
+  static constexpr int cs(int j) { return Geo<L, J>::hoff(j + 1) + (j - 1) * C + 1; }
+  static constexpr int total = H + J * C + 2;  // doubles
+};
+
+__device__ __forceinline__ d2 bload2(rsrc_t r, int off) {
+  return __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ void bstore2(rsrc_t r, int off, d2 v) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
+}
+
 template <int L, int J, bool FMA, int NT, class Fetch>
-__device__ __forceinline__ void fwd_step(double* lds, double (&cur)[kC / NT], Fetch&& fetch,
-                                         long a, long P, long seg_end,
-                                         const rsrc_t (&rw)[J + 1], const Taps& taps) {
-  using G = Geo<L, J>;
-  constexpr int R = kC / NT;
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int r = 0; r < R; ++r) lds[G::fwd_off(1) + G::hist(1) + tid + r * NT] = cur[r];
+__device__ __forceinline__ void fwd_step(double* lds, d2& cur, Fetch&& fetch, long a, long P,
+                                         long seg_end, const rsrc_t (&rw)[J + 1],
+                                         const Taps& taps) {
+  constexpr int C = 2 * NT;
+  using G = GeoF<L, J, C>;
+  const int t = threadIdx.x;
+  const int i = 2 * t;
+  *(d2*)&lds[G::cs(1) + i] = cur;
   fetch(cur);  // the chunk two steps ahead: in flight behind this step and the next
   __syncthreads();
+  const long pos = a + i;
+  const int off = (pos >= P && pos < seg_end) ? (int)(pos * 8) : kOOB;  // P, seg_end even
 #pragma unroll
   for (int j = 1; j <= J; ++j) {
     const int d = 1 << (j - 1);
-    const double* src = lds + G::fwd_off(j) + G::hist(j);
+    const double* src = lds + G::cs(j);
+    double w0 = 0.0, v0 = 0.0, w1 = 0.0, v1 = 0.0;  // outputs i and i+1
+    if (d == 1) {
+      d2 pr[L / 2 + 1];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int i = tid + r * NT;
-      double w = 0.0, v = 0.0;
+      for (int q = 0; q <= L / 2; ++q) pr[q] = *(const d2*)&src[i - 2 * q];
 #pragma unroll
       for (int m = 0; m < L; ++m) {
-        const double xv = src[i - m * d];
-        w = madd<FMA>(w, taps.b[m], xv);
-        v = madd<FMA>(v, taps.a[m], xv);
+        // x[i - m] = v[m+1], x[i + 1 - m] = v[m], v[k] = k even ? pr[k/2].y : pr[(k-1)/2].x
+        const double lo = ((m + 1) & 1) ? pr[m / 2].x : pr[(m + 1) / 2].y;
+        const double hi = (m & 1) ? pr[(m - 1) / 2].x : pr[m / 2].y;
+        w0 = madd<FMA>(w0, taps.b[m], lo);
+        v0 = madd<FMA>(v0, taps.a[m], lo);
+        w1 = madd<FMA>(w1, taps.b[m], hi);
+        v1 = madd<FMA>(v1, taps.a[m], hi);
       }
-      const long pos = a + i;
-      const int off = (pos >= P && pos < seg_end) ? (int)(pos * 8) : kOOB;
-      bstore(rw[j - 1], off, w);
-      if (j < J) {
-        lds[G::fwd_off(j + 1) + G::hist(j + 1) + i] = v;
-      } else {
-        bstore(rw[J], off, v);
+    } else {
+#pragma unroll
+      for (int m = 0; m < L; ++m) {
+        const d2 pr = *(const d2*)&src[i - m * d];
+        w0 = madd<FMA>(w0, taps.b[m], pr.x);
+        v0 = madd<FMA>(v0, taps.a[m], pr.x);
+        w1 = madd<FMA>(w1, taps.b[m], pr.y);
+        v1 = madd<FMA>(v1, taps.a[m], pr.y);
       }
+    }
+    bstore2(rw[j - 1], off, d2{w0, w1});
+    if (j < J) {
+      *(d2*)&lds[G::cs(j + 1) + i] = d2{v0, v1};
+    } else {
+      bstore2(rw[J], off, d2{v0, v1});
     }
     __syncthreads();
   }
-  // History shift B_{j-1}[C .. C+hist_j) -> [0 .. hist_j): flat e -> src e + j*C, dst e + (j-1)*C.
+  // History shift: level j's last hist_j samples [C - hist_j, C) move to [-hist_j, 0).  Flat
+  // e over H: src e + j*C + 1, dst e + (j-1)*C + 1 (see GeoF).
   constexpr int kPer = (G::H + NT - 1) / NT;
   if constexpr (kPer > 0) {
     double hv[kPer];
 #pragma unroll
     for (int r = 0; r < kPer; ++r) {
-      const int e = tid + r * NT;
-      if (e < G::H) hv[r] = lds[e + level_of<L>(e) * kC];
+      const int e = t + r * NT;
+      if (e < G::H) hv[r] = lds[e + level_of<L>(e) * C + 1];
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kPer; ++r) {
-      const int e = tid + r * NT;
-      if (e < G::H) lds[e + (level_of<L>(e) - 1) * kC] = hv[r];
+      const int e = t + r * NT;
+      if (e < G::H) lds[e + (level_of<L>(e) - 1) * C + 1] = hv[r];
     }
   }
 }
@@ -137,9 +172,9 @@ __global__ __launch_bounds__(NT) void modwt_fwd_fast(const double* __restrict__ 
                                                      long seg_len, long warm, long npairs,
                                                      Taps taps) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  using G = Geo<L, J>;
-  constexpr int R = kC / NT;
-  const int tid = threadIdx.x;
+  constexpr int C = 2 * NT;
+  using G = GeoF<L, J, C>;
+  const int t = threadIdx.x;
   const long P = (long)blockIdx.x * seg_len;
   const long seg_end = min(P + seg_len, N);
   const double* xs = x + (long)blockIdx.y * N;
@@ -148,22 +183,19 @@ __global__ __launch_bounds__(NT) void modwt_fwd_fast(const double* __restrict__ 
   rsrc_t rw[J + 1];
 #pragma unroll
   for (int j = 0; j <= J; ++j) rw[j] = make_rsrc(cs + (long)j * N, N);
-  for (int i = tid; i < G::fwd_total; i += NT) lds[i] = 0.0;
+  for (int i = t; i < G::total; i += NT) lds[i] = 0.0;
 
   long a = P - warm;
-  long lb = a % N;  // load cursor: stream position of the next chunk to fetch, mod N
+  long lb = a % N;  // load cursor: stream position of the next chunk to fetch, mod N (even)
   if (lb < 0) lb += N;
-  auto fetch = [&](double (&dst)[R]) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      long p = lb + tid + r * NT;
-      p = p >= N ? p - N : p;
-      dst[r] = bload(rx, (int)(p * 8));
-    }
-    lb += kC;
+  auto fetch = [&](d2& dst) {
+    long p = lb + 2 * t;
+    p = p >= N ? p - N : p;
+    dst = bload2(rx, (int)(p * 8));
+    lb += C;
     if (lb >= N) lb -= N;
   };
-  double A[R], B[R];
+  d2 A, B;
   fetch(A);
   __builtin_amdgcn_sched_barrier(0);  // keep A's loads strictly older than B's (counted waits)
   fetch(B);
@@ -172,13 +204,13 @@ __global__ __launch_bounds__(NT) void modwt_fwd_fast(const double* __restrict__ 
   // loop back-edge (two steps of stores + one fetch behind A), so the compiler's merged wait
   // at the first step is the steady-state counted vmcnt, not a near-drain.
 #pragma unroll
-  for (int i = 0; i < 2 * R * (J + 1); ++i) bstore(rx, kOOB - 8 * i, 0.0);  // distinct: not merged
+  for (int k = 0; k < 2 * (J + 1); ++k) bstore(rx, kOOB - 8 * k, 0.0);  // distinct: not merged
   __syncthreads();
   for (long k = 0; k < npairs; ++k) {
     fwd_step<L, J, FMA, NT>(lds, A, fetch, a, P, seg_end, rw, taps);
-    a += kC;
+    a += C;
     fwd_step<L, J, FMA, NT>(lds, B, fetch, a, P, seg_end, rw, taps);
-    a += kC;
+    a += C;
   }
 }
 
@@ -248,7 +280,7 @@ __device__ __forceinline__ void inv_step(d2* vw, double (&cur)[(C / NT) * (J + 1
   }
 }
 
-template <int L, int J, bool FMA, int C, int NT>
+template <int L, int J, bool FMA, int C, int NT, int D>
 __global__ __launch_bounds__(NT) void modwt_inv_fast(const double* __restrict__ coeffs,
                                                      double* __restrict__ x, long N,
                                                      long seg_len, long a_start, long npairs,
@@ -280,19 +312,23 @@ __global__ __launch_bounds__(NT) void modwt_inv_fast(const double* __restrict__ 
     lb -= C;
     if (lb < 0) lb += N;
   };
-  double A[R * (J + 1)], B[R * (J + 1)];
-  fetch(A);
-  __builtin_amdgcn_sched_barrier(0);  // keep A's loads strictly older than B's (counted waits)
-  fetch(B);
-  __builtin_amdgcn_sched_barrier(0);
+  // D register sets: the chunk of step s is fetched at the top of step s - D + ... so D-1
+  // whole steps of work hide each load.
+  double S[D][R * (J + 1)];
 #pragma unroll
-  for (int i = 0; i < 2 * R; ++i) bstore(rx, kOOB - 8 * i, 0.0);  // queue-depth padding
+  for (int q = 0; q < D; ++q) {
+    fetch(S[q]);
+    __builtin_amdgcn_sched_barrier(0);  // set q's loads strictly older than set q+1's
+  }
+#pragma unroll
+  for (int i = 0; i < D * R; ++i) bstore(rx, kOOB - 8 * i, 0.0);  // queue-depth padding
   __syncthreads();
-  for (long k = 0; k < npairs; ++k) {
-    inv_step<L, J, FMA, C, NT>((d2*)lds, A, fetch, a, P, seg_end, rx, taps);
-    a -= C;
-    inv_step<L, J, FMA, C, NT>((d2*)lds, B, fetch, a, P, seg_end, rx, taps);
-    a -= C;
+  for (long k = 0; k < npairs; ++k) {  // npairs counts groups of D steps
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      inv_step<L, J, FMA, C, NT>((d2*)lds, S[q], fetch, a, P, seg_end, rx, taps);
+      a -= C;
+    }
   }
 }
 
@@ -301,7 +337,8 @@ __global__ __launch_bounds__(NT) void modwt_inv_fast(const double* __restrict__ 
 // ---------------------------------------------------------------------------------------
 template <int L, int J>
 constexpr bool fwd_ok() {
-  return (size_t)Geo<L, J>::fwd_total * 8 <= 80 * 1024 && Geo<L, J>::H <= 16 * 256;
+  return (size_t)GeoF<L, J, 512>::total * 8 <= 80 * 1024 && Geo<L, J>::H <= 16 * 256 &&
+         L % 2 == 0;
 }
 template <int L, int J, int C>
 constexpr bool inv_fits() {
@@ -352,33 +389,31 @@ int launch(K kern, size_t lds, long nseg, int batch, int nt, hipStream_t s, cons
 
 template <int L, int J, bool FMA>
 int launch_fwd(const Taps& t, const double* x, double* c, long N, int batch, hipStream_t s) {
-  using G = Geo<L, J>;
-  const long warm = ((long)(G::H + kC - 1) / kC) * kC;
-  const long seg = pick_seg(N, batch, warm);
+  constexpr int NT = 256, C = 2 * NT;
+  using G = GeoF<L, J, C>;
+  const long warm = ((long)(G::H + C - 1) / C) * C;
+  const long seg = pick_seg(N, batch, warm, C);
   const long nseg = (N + seg - 1) / seg;
-  const long npairs = ((seg + warm) / kC + 1) / 2;  // an odd extra step runs right of the segment
-  const size_t lds = (size_t)G::fwd_total * sizeof(double);
+  const long npairs = ((seg + warm) / C + 1) / 2;  // an odd extra step runs right of the segment
+  const size_t lds = (size_t)G::total * sizeof(double);
   const long cs = (long)(J + 1) * N;
-  if (pick_nt("JW_FWD_NT", 256) == 512)
-    return launch(modwt_fwd_fast<L, J, FMA, 512>, lds, nseg, batch, 512, s, x, N, c, cs, N, seg,
-                  warm, npairs, t);
-  return launch(modwt_fwd_fast<L, J, FMA, 256>, lds, nseg, batch, 256, s, x, N, c, cs, N, seg,
-                warm, npairs, t);
+  return launch(modwt_fwd_fast<L, J, FMA, NT>, lds, nseg, batch, NT, s, x, N, c, cs, N, seg, warm,
+                npairs, t);
 }
 
-template <int L, int J, bool FMA, int C>
+template <int L, int J, bool FMA, int C, int D>
 int launch_inv_c(const Taps& t, const double* c, double* x, long N, int batch, hipStream_t s) {
   using G = GeoI<L, J, C>;
   const long warm = ((long)(G::H + C - 1) / C) * C;
   const long seg = pick_seg(N, batch, warm, C);
   const long nseg = (N + seg - 1) / seg;
   const long steps = seg / C + warm / C;
-  const long npairs = (steps + 1) / 2;
-  const long a_start = (steps - 1) * C;  // an odd extra step runs left of the segment
+  const long ngroups = (steps + D - 1) / D;
+  const long a_start = (steps - 1) * C;  // surplus steps (to a multiple of D) run left of the segment
   const size_t lds = (size_t)G::inv_total * sizeof(double);
   const long cs = (long)(J + 1) * N;
-  return launch(modwt_inv_fast<L, J, FMA, C, C>, lds, nseg, batch, C, s, c, cs, x, N, N, seg,
-                a_start, npairs, t);
+  return launch(modwt_inv_fast<L, J, FMA, C, C, D>, lds, nseg, batch, C, s, c, cs, x, N, N, seg,
+                a_start, ngroups, t);
 }
 
 // Inverse chunk (= threads per workgroup, one sample each per level): 256 (measured best
@@ -387,13 +422,13 @@ template <int L, int J, bool FMA>
 int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hipStream_t s) {
   const char* e = std::getenv("JW_INV_C");
   const int want = e ? std::atoi(e) : 256;
-  if constexpr (inv_fits<L, J, 512>()) {
-    if (want == 512) return launch_inv_c<L, J, FMA, 512>(t, c, x, N, batch, s);
-  }
+  const char* ed = std::getenv("JW_INV_D");
+  const int depth = ed ? std::atoi(ed) : 2;
   if constexpr (inv_fits<L, J, 384>()) {
-    if (want == 384) return launch_inv_c<L, J, FMA, 384>(t, c, x, N, batch, s);
+    if (want == 384) return launch_inv_c<L, J, FMA, 384, 2>(t, c, x, N, batch, s);
   }
-  return launch_inv_c<L, J, FMA, 256>(t, c, x, N, batch, s);
+  if (depth == 3) return launch_inv_c<L, J, FMA, 256, 3>(t, c, x, N, batch, s);
+  return launch_inv_c<L, J, FMA, 256, 2>(t, c, x, N, batch, s);
 }
 
 // Returned when (L, J, N) has no fast kernel (the caller falls back to the generic ones).
@@ -402,7 +437,7 @@ constexpr int kNotHandled = -100;
 template <int L>
 int forward(const Taps& t, bool fma, const double* x, double* c, long N, int J, int batch,
             hipStream_t s) {
-  if (N < kC || N >= (1L << 27)) return kNotHandled;
+  if (N < kC || (N & 1) || N >= (1L << 27)) return kNotHandled;
   int st = kNotHandled;
   auto one = [&](auto jc) {
     constexpr int JJ = decltype(jc)::value;

@@ -7,8 +7,8 @@ TAG="$1"; shift
 OUT="gpurun_out/sweep_$TAG.log"
 : > "$OUT"
 for arith in fma strict; do
-  for ic in 256 384 512; do
-    JW_INV_C=$ic timeout -k 10 300 python bench.py --steps 6 --warmup 2 \
+  for ic in 256 384 d3; do
+    JW_INV_C=${ic/d3/256} JW_INV_D=$([ $ic = d3 ] && echo 3 || echo 2) timeout -k 10 300 python bench.py --steps 6 --warmup 2 \
         --arith $arith --no-cpu-baseline --no-check "$@" > /tmp/sw.json 2>/dev/null
     rc=$?
     if [ $rc -ne 0 ]; then echo "variant $arith $ic rc=$rc" >> "$OUT"; cat "$OUT"; exit $rc; fi
