@@ -41,7 +41,9 @@ def parse():
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--levels", type=int, default=8)
     ap.add_argument("--wavelet", default="Daubechies4")
-    ap.add_argument("--arith", choices=["strict", "fma"], default="strict")
+    ap.add_argument("--arith", choices=["strict", "fma"], default="fma",
+                    help="headline arithmetic; the other contract is timed too and reported")
+    ap.add_argument("--no-alt", action="store_true", help="skip timing the other arith mode")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
     return ap.parse_args()
@@ -55,7 +57,8 @@ def cpu_baseline(wname, n, J, threads):
     g, h = orc.modwt_filters(wv.getScalingDeComposition(), wv.getWaveletDeComposition())
     # AUTO-faithful: at N=2^20 JWave's default performConvolution picks the FFT path for
     # every level (N*M_j > 4096, MODWTTransform.java:653) -- recurrence-twiddle radix-2 FFT.
-    xs = orc.fill_uniform(threads * n, 42).reshape(threads, n)
+    ns = 2 * threads  # two signals per thread: ~10-15 s of CPU work on the box
+    xs = orc.fill_uniform(ns * n, 42).reshape(ns, n)
     t0 = time.perf_counter()
     orc.modwt_fwdinv_batch(xs, J, g, h, use_fft=True, threads=threads)
     t_auto = time.perf_counter() - t0
@@ -63,15 +66,15 @@ def cpu_baseline(wname, n, J, threads):
     # its cost per sample does not depend on N.
     nd = n // 4
     t0 = time.perf_counter()
-    orc.modwt_fwdinv_batch(xs[:, :nd].copy(), J, g, h, use_fft=False, threads=threads)
+    orc.modwt_fwdinv_batch(xs[:threads, :nd].copy(), J, g, h, use_fft=False, threads=threads)
     t_direct = time.perf_counter() - t0
     return {
-        "value": threads * n / t_auto / 1e6,
+        "value": ns * n / t_auto / 1e6,
         "unit": "Msamples/s",
         "cores": threads,
         "kind": "port",
-        "sample": (f"{threads} signals x N={n} {wname} J={J} fwd+inv, AUTO path as JWave runs it "
-                   f"(FFT convolution, MODWTTransform.java:653), OpenMP over signals: "
+        "sample": (f"{ns} signals x N={n} {wname} J={J} fwd+inv, AUTO path as JWave runs it "
+                   f"(FFT convolution, MODWTTransform.java:653), OpenMP over signals on {threads} threads: "
                    f"{t_auto:.2f} s; DIRECT-faithful on {threads} x N={nd}: "
                    f"{threads * nd / t_direct / 1e6:.3f} Msamples/s"),
         "direct_value": threads * nd / t_direct / 1e6,
@@ -86,63 +89,89 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        from jwave import distributed as jdist
+        jdist.init_from_env("nccl", device=dev)
 
     from jwave import MODWTTransform, _native
     from jwave.transforms import wavelets as W
 
     B, n, J = args.batch, args.n, args.levels
     wv = W.by_name(args.wavelet)
-    m = MODWTTransform(wv, arith=args.arith)
-    m.setConvolutionMethod(MODWTTransform.ConvolutionMethod.DIRECT)
     lib = _native.lib()
     stream = torch.cuda.current_stream(dev)
     sptr = ctypes.c_void_p(stream.cuda_stream)
-    plan = m.initializeFilterCache()
 
     x = torch.empty((B, n), dtype=torch.float64, device=dev)
     c = torch.empty((B, J + 1, n), dtype=torch.float64, device=dev)
     xr = torch.empty((B, n), dtype=torch.float64, device=dev)
-    seed0 = 42 + rank * B  # global signal index g -> java.util.Random(42 + g)
+    seed0 = 42 + rank * B  # weak scaling: rank r owns global signals [r*B, (r+1)*B), seed 42 + g
     _native.check(lib.jw_synth_uniform(ctypes.c_void_p(x.data_ptr()), n, B, seed0, sptr))
 
-    def fwd():
-        _native.check(lib.jw_modwt_forward(plan, ctypes.c_void_p(x.data_ptr()),
-                                           ctypes.c_void_p(c.data_ptr()), n, J, B,
-                                           _native.JW_CONV_DIRECT, _native.JW_DEVICE, sptr))
+    def run(arith, steps, warmup):
+        """Time `steps` fwd+inv steps; returns (elapsed_s max over ranks, fwd_ms, inv_ms)."""
+        m = MODWTTransform(wv, arith=arith)
+        m.setConvolutionMethod(MODWTTransform.ConvolutionMethod.DIRECT)
+        plan = m.initializeFilterCache()
 
-    def inv():
-        _native.check(lib.jw_modwt_inverse(plan, ctypes.c_void_p(c.data_ptr()),
-                                           ctypes.c_void_p(xr.data_ptr()), n, J, B,
-                                           _native.JW_CONV_DIRECT, _native.JW_DEVICE, sptr))
+        def fwd():
+            _native.check(lib.jw_modwt_forward(plan, ctypes.c_void_p(x.data_ptr()),
+                                               ctypes.c_void_p(c.data_ptr()), n, J, B,
+                                               _native.JW_CONV_DIRECT, _native.JW_DEVICE, sptr))
 
-    for _ in range(args.warmup):
-        fwd()
-        inv()
-    torch.cuda.synchronize()
+        def inv():
+            _native.check(lib.jw_modwt_inverse(plan, ctypes.c_void_p(c.data_ptr()),
+                                               ctypes.c_void_p(xr.data_ptr()), n, J, B,
+                                               _native.JW_CONV_DIRECT, _native.JW_DEVICE, sptr))
 
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        ev[k][0].record(stream)
-        fwd()
-        ev[k][1].record(stream)
-        inv()
-        ev[k][2].record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+        for _ in range(warmup):
+            fwd()
+            inv()
+        torch.cuda.synchronize()
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            ev[k][0].record(stream)
+            fwd()
+            ev[k][1].record(stream)
+            inv()
+            ev[k][2].record(stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            from jwave import distributed as jdist
+            elapsed = jdist.max_over_ranks(elapsed, device=dev)
+        fwd_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / steps
+        inv_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / steps
+        return elapsed, fwd_ms, inv_ms
 
-    fwd_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
-    inv_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps
+    def spot_check(arith):
+        """One signal's coefficients against the oracle (bit-exact for strict)."""
+        import numpy as np
+        import oracle as orc
+        g, h = orc.modwt_filters(wv.getScalingDeComposition(), wv.getWaveletDeComposition())
+        sig = min(1, B - 1)
+        ref = orc.modwt_forward(orc.fill_uniform(n, seed0 + sig), J, g, h, "direct_nz")
+        got = c[sig].cpu().numpy()
+        if arith == "strict":
+            return "bit-exact" if np.array_equal(got.view(np.uint64), ref.view(np.uint64)) else \
+                f"MISMATCH max {float(np.max(np.abs(got - ref)))}"
+        return f"normwise {float(np.max(np.abs(got - ref)) / np.max(np.abs(ref))):.2e}"
+
+    alt_arith = "strict" if args.arith == "fma" else "fma"
+    alt = None
+    if not args.no_alt:
+        a_el, a_f, a_i = run(alt_arith, max(2, args.steps // 2), 1)
+        alt = {"arith": alt_arith, "value": round(B * n * world / (a_el / max(2, args.steps // 2)) / 1e6, 1),
+               "fwd_ms": round(a_f, 3), "inv_ms": round(a_i, 3)}
+        if rank == 0 and not args.no_check:
+            alt["spot_check_vs_oracle"] = spot_check(alt_arith)
+
+    elapsed, fwd_ms, inv_ms = run(args.arith, args.steps, args.warmup)
     ms_per_step = elapsed * 1e3 / args.steps
     total_samples = B * n * world
     value = total_samples / (elapsed / args.steps) / 1e6
@@ -151,9 +180,9 @@ def main():
     err = ((xr - x).abs().amax() / x.abs().amax()).item()
     rms = torch.sqrt(torch.mean((xr - x) ** 2)).item()
     if world > 1:
-        t = torch.tensor([err, rms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        err, rms = t[0].item(), t[1].item()
+        from jwave import distributed as jdist
+        err = jdist.max_over_ranks(err, device=dev)
+        rms = jdist.max_over_ranks(rms, device=dev)
 
     if rank == 0:
         # Roofline of the dominant kernel: algorithmic bytes per launch / average launch time.
@@ -170,19 +199,7 @@ def main():
                 traffic = tr.get(key, {}).get(name)
             except Exception:
                 traffic = None
-        check = None
-        if not args.no_check:
-            import numpy as np
-            import oracle as orc
-            g, h = orc.modwt_filters(wv.getScalingDeComposition(), wv.getWaveletDeComposition())
-            sig = min(1, B - 1)
-            ref = orc.modwt_forward(orc.fill_uniform(n, seed0 + sig), J, g, h, "direct_nz")
-            got = c[sig].cpu().numpy()
-            if args.arith == "strict":
-                check = "bit-exact" if np.array_equal(got.view(np.uint64), ref.view(np.uint64)) else \
-                    f"MISMATCH max {float(np.max(np.abs(got - ref)))}"
-            else:
-                check = f"normwise {float(np.max(np.abs(got - ref)) / np.max(np.abs(ref))):.2e}"
+        check = None if args.no_check else spot_check(args.arith)
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -212,8 +229,14 @@ def main():
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": per_launch,
                 "fwd_ms": round(fwd_ms, 3), "inv_ms": round(inv_ms, 3),
+                "step_achieved": round(2 * per_launch / ((fwd_ms + inv_ms) * 1e-3) / 1e9, 1),
+                "step_frac": round(2 * per_launch / ((fwd_ms + inv_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "note": ("achieved = algorithmic bytes per launch (8*(1+(J+1)) B/sample x B*N) / "
+                         "average launch time from HIP events on the launch stream; traffic = "
+                         "rocprofv3 FETCH_SIZE*2 + WRITE_SIZE per launch (profiles/)"),
             },
             "cpu_baseline": None,
+            "other_arith": alt,
         }
         if world == 1 and not args.no_cpu_baseline:
             threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)

@@ -9,13 +9,13 @@ timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x > gpur
 rc=$?
 echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu_$TAG.log
 if [ $rc -gt 1 ]; then exit $rc; fi
-timeout -k 10 600 python bench.py --steps 10 --warmup 2 > gpurun_out/bench_$TAG.log 2>&1
+timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.log 2>&1
 rc=$?
 echo "bench rc=$rc"; tail -3 gpurun_out/bench_$TAG.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$TAG" -o run --output-format csv \
-  -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-check > "$R/gpurun_out/prof_$TAG.log" 2>&1
+  -- python3 "$R/bench.py" > "$R/gpurun_out/prof_$TAG.log" 2>&1
 rc=$?
 echo "rocprof rc=$rc"; tail -2 "$R/gpurun_out/prof_$TAG.log"
 exit $rc

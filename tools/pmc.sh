@@ -7,13 +7,14 @@ mkdir -p "$R/gpurun_out/pmc_$TAG"
 cd /tmp && export TMPDIR=/tmp
 i=0
 for ctrs in "FETCH_SIZE" "WRITE_SIZE" \
-            "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS" \
-            "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE"; do
+            "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU" \
+            "SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM_RD SQ_LDS_UNALIGNED_STALL SQ_LDS_DATA_FIFO_FULL SQ_LDS_CMD_FIFO_FULL GRBM_GUI_ACTIVE" \
+            "TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TA_BUSY_avr TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum"; do
   i=$((i+1))
   timeout -k 10 400 rocprofv3 --kernel-trace --pmc $ctrs -d "$R/gpurun_out/pmc_$TAG/p$i" -o run \
       --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline --no-check "$@" \
       > "$R/gpurun_out/pmc_$TAG/p$i.log" 2>&1
   rc=$?
-  echo "pass $i ($ctrs) rc=$rc"
+  echo "pass $i rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$R/gpurun_out/pmc_$TAG/p$i.log"; exit $rc; fi
 done
