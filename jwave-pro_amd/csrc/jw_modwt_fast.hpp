@@ -23,6 +23,9 @@
 namespace jw {
 namespace fast {
 
+#ifndef JW_INV_SYNC
+#define JW_INV_SYNC() __syncthreads()  // (microbenchmarks redefine it to time the barriers)
+#endif
 constexpr int kC = 512;           // samples per level per step (both directions)
 constexpr int kOOB = 0x7ffff000;  // byte offset beyond any row (N < 2^27): store dropped
 
@@ -217,70 +220,129 @@ __global__ __launch_bounds__(NT) void modwt_fwd_fast(const double* __restrict__ 
 // ---------------------------------------------------------------------------------------
 // Inverse: right -> left.  VW_j holds (V_j, W_j) pairs at positions [a, a + C + hist_j);
 // thread t owns samples t + r*NT.  cur[(J+1)*r + (j-1)] = W_j, cur[(J+1)*r + J] = V_J.
+// Levels j >= RF (dilation >= 64) are ring buffers of S_j = C + hist_j pairs (position a + u
+// lives at (rb[j] + u) mod S_j, rb[j] steps back by C per chunk): no history shift.  Levels
+// below RF keep [chunk | history] linear and shift the history.
 // ---------------------------------------------------------------------------------------
-template <int L, int J, bool FMA, int C, int NT, class Fetch>
+template <int L, int J, int C, int RF>
+struct Ring {
+  static_assert(RF > J || ((1 << (RF - 1)) >= 64 && C % 64 == 0), "ring levels need d >= 64");
+  static constexpr bool on(int j) { return j >= RF; }
+  static constexpr int S(int j) { return C + Geo<L, J>::hist(j); }
+  static constexpr int shifted() {  // pairs of flat history that still shift (levels < RF)
+    return RF > J ? Geo<L, J>::H : Geo<L, J>::hoff(RF);
+  }
+  // Every shifted level's history fits beside its chunk (hist_j <= C): level j's shift
+  // [0, hist_j) -> [C, C + hist_j) then runs inside level j-1's phase (level 1's at the next
+  // step's first phase) instead of a separate two-barrier phase.
+  static constexpr bool inline_shift() {
+    return J >= 2 && Geo<L, J>::hist(RF > J ? J : RF - 1 < 1 ? 1 : RF - 1) <= C;
+  }
+};
+
+// Ring index of window position u = ub + lane, with ub wave-uniform.  Ring levels have a
+// dilation >= 64 and C, NT are multiples of 64, so S_j, rb_j and ub are all multiples of 64
+// and a wave's 64 lanes never straddle the ring's end: the wrap is decided once per wave on
+// the scalar unit and costs one vector add per access.
+template <int L, int J, int C, int RF>
+__device__ __forceinline__ int ring_idx(int j, const int (&rb)[J + 1], int ub, int lane) {
+  using Rg = Ring<L, J, C, RF>;
+  int x = rb[j] + ub;  // uniform, multiple of 64, < 2 S_j
+  x = x >= Rg::S(j) ? x - Rg::S(j) : x;
+  return x + lane;
+}
+
+template <int L, int J, bool FMA, int C, int NT, int RF, class Fetch>
 __device__ __forceinline__ void inv_step(d2* vw, double (&cur)[(C / NT) * (J + 1)],
                                          Fetch&& fetch, long a, long P, long seg_end,
-                                         const rsrc_t& rx, const Taps& taps) {
+                                         const rsrc_t& rx, const Taps& taps, int (&rb)[J + 1]) {
   using G = GeoI<L, J, C>;
+  using Rg = Ring<L, J, C, RF>;
   constexpr int R = C / NT;
   const int t = threadIdx.x;
   // W_j samples of this step stay in registers until V_j is known (level j+1), so every
   // (V_j, W_j) pair reaches LDS as one 16-byte store (8-byte stores at a 16-byte stride
   // would conflict 2-way).
   double wj[R][J];
+  const int lane = t & 63;
+  const int w64 = __builtin_amdgcn_readfirstlane(t & ~63);  // wave-uniform part of t
+  auto ridx = [&](int j, int ubase, int u) {  // u = ubase + lane; non-ring levels use u as is
+    return Rg::on(j) ? ring_idx<L, J, C, RF>(j, rb, ubase, lane) : u;
+  };
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    vw[G::inv_off(J) + t + r * NT] = d2{cur[(J + 1) * r + J], cur[(J + 1) * r + J - 1]};
+    vw[G::inv_off(J) + ridx(J, w64 + r * NT, t + r * NT)] =
+        d2{cur[(J + 1) * r + J], cur[(J + 1) * r + J - 1]};
 #pragma unroll
     for (int j = 1; j < J; ++j) wj[r][j] = cur[(J + 1) * r + j - 1];
   }
+  // Inline history shift of linear level jj (see Ring::inline_shift).
+  auto shift_level = [&](int jj) {
+    if (jj < 1 || jj > J || Rg::on(jj)) return;
+    const int hj = Geo<L, J>::hist(jj);
+#pragma unroll
+    for (int e0 = 0; e0 < C; e0 += NT) {
+      const int e = e0 + t;
+      if (e < hj) vw[G::inv_off(jj) + C + e] = vw[G::inv_off(jj) + e];
+    }
+  };
+  constexpr bool kInline = Rg::inline_shift();
+  if constexpr (kInline) shift_level(1);  // level 1's chunk of the previous step
   fetch(cur);  // the chunk two steps ahead
-  __syncthreads();
+  JW_INV_SYNC();
 #pragma unroll
   for (int j = J; j >= 1; --j) {
     const int d = 1 << (j - 1);
     const d2* src = vw + G::inv_off(j);
+    if constexpr (kInline) shift_level(j + 1);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int i = t + r * NT;
       double ap = 0.0, dp = 0.0;
 #pragma unroll
       for (int m = 0; m < L; ++m) {
-        const d2 p = src[i + m * d];
+        const d2 p = src[ridx(j, w64 + r * NT + m * d, i + m * d)];
         ap = madd<FMA>(ap, taps.a[m], p.x);
         dp = madd<FMA>(dp, taps.b[m], p.y);
       }
       const double v = ap + dp;  // inverseMODWT :366-369, vFromApprox + vFromDetail
       if (j > 1) {
-        vw[G::inv_off(j - 1) + i] = d2{v, wj[r][j - 1]};
+        vw[G::inv_off(j - 1) + ridx(j - 1, w64 + r * NT, i)] = d2{v, wj[r][j - 1]};
       } else {
         const long pos = a + i;
         bstore(rx, (pos >= P && pos < seg_end) ? (int)(pos * 8) : kOOB, v);
       }
     }
-    __syncthreads();
+    JW_INV_SYNC();
   }
-  // History shift of every VW_j: [0 .. hist_j) -> [C .. C + hist_j) (flat e over H pairs:
-  // src e + (j-1)*C, dst e + j*C).
-  constexpr int kPer = (G::H + NT - 1) / NT;
+  // History shift of the linear levels: [0 .. hist_j) -> [C .. C + hist_j) (flat e over
+  // their pairs: src e + (j-1)*C, dst e + j*C).
+  constexpr int HS = kInline ? 0 : Rg::shifted();
+  constexpr int kPer = (HS + NT - 1) / NT;
   if constexpr (kPer > 0) {
     d2 hv[kPer];
 #pragma unroll
     for (int r = 0; r < kPer; ++r) {
       const int e = t + r * NT;
-      if (e < G::H) hv[r] = vw[e + (level_of<L>(e) - 1) * C];
+      if (e < HS) hv[r] = vw[e + (level_of<L>(e) - 1) * C];
     }
-    __syncthreads();
+    JW_INV_SYNC();
 #pragma unroll
     for (int r = 0; r < kPer; ++r) {
       const int e = t + r * NT;
-      if (e < G::H) vw[e + level_of<L>(e) * C] = hv[r];
+      if (e < HS) vw[e + level_of<L>(e) * C] = hv[r];
+    }
+  }
+#pragma unroll
+  for (int j = 1; j <= J; ++j) {
+    if (Rg::on(j)) {
+      rb[j] -= C;
+      if (rb[j] < 0) rb[j] += Rg::S(j);
     }
   }
 }
 
-template <int L, int J, bool FMA, int C, int NT, int D>
+template <int L, int J, bool FMA, int C, int NT, int D, int RF>
 __global__ __launch_bounds__(NT) void modwt_inv_fast(const double* __restrict__ coeffs,
                                                      double* __restrict__ x, long N,
                                                      long seg_len, long a_start, long npairs,
@@ -322,11 +384,14 @@ __global__ __launch_bounds__(NT) void modwt_inv_fast(const double* __restrict__ 
   }
 #pragma unroll
   for (int i = 0; i < D * R; ++i) bstore(rx, kOOB - 8 * i, 0.0);  // queue-depth padding
+  int rb[J + 1];
+#pragma unroll
+  for (int j = 0; j <= J; ++j) rb[j] = 0;
   __syncthreads();
   for (long k = 0; k < npairs; ++k) {  // npairs counts groups of D steps
 #pragma unroll
     for (int q = 0; q < D; ++q) {
-      inv_step<L, J, FMA, C, NT>((d2*)lds, S[q], fetch, a, P, seg_end, rx, taps);
+      inv_step<L, J, FMA, C, NT, RF>((d2*)lds, S[q], fetch, a, P, seg_end, rx, taps, rb);
       a -= C;
     }
   }
@@ -360,12 +425,13 @@ inline int pick_nt(const char* env, int dflt) {
 
 // Segment of a signal per workgroup: whole chunks, at least 8x the warm-up, and enough
 // segments that the grid holds several waves of workgroups.
-inline long pick_seg(long N, int batch, long warm, int C = kC) {
+inline long pick_seg(long N, int batch, long warm, int C = kC, long min_wgs = 8192) {
   const long nchunks = (N + C - 1) / C;
   long min_chunks = (8 * warm) / C;
   if (min_chunks < 1) min_chunks = 1;
   long seg_chunks = nchunks;
-  while (seg_chunks > min_chunks && (long)batch * ((nchunks + seg_chunks - 1) / seg_chunks) < 8192)
+  while (seg_chunks > min_chunks &&
+         (long)batch * ((nchunks + seg_chunks - 1) / seg_chunks) < min_wgs)
     seg_chunks = (seg_chunks + 1) / 2;
   if (seg_chunks < min_chunks) seg_chunks = min_chunks < nchunks ? min_chunks : nchunks;
   return seg_chunks * C;
@@ -401,7 +467,7 @@ int launch_fwd(const Taps& t, const double* x, double* c, long N, int batch, hip
                 npairs, t);
 }
 
-template <int L, int J, bool FMA, int C, int D>
+template <int L, int J, bool FMA, int C, int D, int RF>
 int launch_inv_c(const Taps& t, const double* c, double* x, long N, int batch, hipStream_t s) {
   using G = GeoI<L, J, C>;
   const long warm = ((long)(G::H + C - 1) / C) * C;
@@ -412,23 +478,18 @@ int launch_inv_c(const Taps& t, const double* c, double* x, long N, int batch, h
   const long a_start = (steps - 1) * C;  // surplus steps (to a multiple of D) run left of the segment
   const size_t lds = (size_t)G::inv_total * sizeof(double);
   const long cs = (long)(J + 1) * N;
-  return launch(modwt_inv_fast<L, J, FMA, C, C, D>, lds, nseg, batch, C, s, c, cs, x, N, N, seg,
+  return launch(modwt_inv_fast<L, J, FMA, C, C, D, RF>, lds, nseg, batch, C, s, c, cs, x, N, N, seg,
                 a_start, ngroups, t);
 }
 
-// Inverse chunk (= threads per workgroup, one sample each per level): 256 (measured best
-// for db4 J=8: 2 workgroups per CU); env JW_INV_C (256 / 384 / 512) overrides for A/B runs.
+// Inverse chunk C = 256 = threads per workgroup (one sample each per level; measured best
+// for db4 J=8: 2 workgroups per CU), two register sets.  The levels with dilation >= 64
+// (j >= 7) are ring buffers by default; env JW_INV_RING=off shifts every level (A/B runs).
 template <int L, int J, bool FMA>
 int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hipStream_t s) {
-  const char* e = std::getenv("JW_INV_C");
-  const int want = e ? std::atoi(e) : 256;
-  const char* ed = std::getenv("JW_INV_D");
-  const int depth = ed ? std::atoi(ed) : 2;
-  if constexpr (inv_fits<L, J, 384>()) {
-    if (want == 384) return launch_inv_c<L, J, FMA, 384, 2>(t, c, x, N, batch, s);
-  }
-  if (depth == 3) return launch_inv_c<L, J, FMA, 256, 3>(t, c, x, N, batch, s);
-  return launch_inv_c<L, J, FMA, 256, 2>(t, c, x, N, batch, s);
+  const char* e = std::getenv("JW_INV_RING");
+  if (e && e[0] == 'o') return launch_inv_c<L, J, FMA, 256, 2, J + 1>(t, c, x, N, batch, s);
+  return launch_inv_c<L, J, FMA, 256, 2, (J >= 7 ? 7 : J + 1)>(t, c, x, N, batch, s);
 }
 
 // Returned when (L, J, N) has no fast kernel (the caller falls back to the generic ones).

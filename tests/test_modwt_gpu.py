@@ -74,6 +74,24 @@ def test_generic_kernels_bit_exact(wname, n, J, monkeypatch):
     assert bits_equal(m.inverseMODWT(ref), orc.modwt_inverse(ref, g, h, "direct_nz"))
 
 
+@pytest.mark.parametrize("ring", ["wave", "off"])
+@pytest.mark.parametrize("wname,n,J", [("Daubechies4", 70001, 8), ("Haar1", 50000, 10),
+                                       ("Symlet8", 20000, 6), ("Daubechies2", 1000, 9),
+                                       ("Daubechies8", 30001, 7), ("Daubechies10", 3000, 4),
+                                       ("Daubechies4", 1 << 16, 10)])
+def test_inverse_kernel_variants_bit_exact(wname, n, J, ring, monkeypatch):
+    # JW_INV_RING=off shifts the history of every level instead of ring-buffering the levels
+    # with dilation >= 64; both must give the same bits
+    wv = W.by_name(wname)
+    g, h = ofilters(wv)
+    c = orc.modwt_forward(orc.fill_uniform(n, 11 + n), J, g, h, "direct_nz")
+    monkeypatch.setenv("JW_INV_RING", ring)
+    ref = orc.modwt_inverse(c, g, h, "direct_nz")
+    assert bits_equal(MODWTTransform(wv).inverseMODWT(c), ref)
+    xr = MODWTTransform(wv, arith="fma").inverseMODWT(c)
+    assert normwise(xr, ref) < FMA_TOL
+
+
 @pytest.mark.parametrize("wname,n,J", [("Haar1", 64, 6), ("Daubechies4", 100, 5),
                                        ("Symlet8", 8, 3), ("Daubechies8", 300, 4)])
 def test_strict_bit_exact_vs_faithful_oracle(wname, n, J):

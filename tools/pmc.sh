@@ -11,6 +11,7 @@ for ctrs in "FETCH_SIZE" "WRITE_SIZE" \
             "SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM_RD SQ_LDS_UNALIGNED_STALL SQ_LDS_DATA_FIFO_FULL SQ_LDS_CMD_FIFO_FULL GRBM_GUI_ACTIVE" \
             "TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TA_BUSY_avr TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum"; do
   i=$((i+1))
+  case " ${PMC_PASSES:-1 2 3 4 5} " in *" $i "*) ;; *) continue ;; esac
   timeout -k 10 400 rocprofv3 --kernel-trace --pmc $ctrs -d "$R/gpurun_out/pmc_$TAG/p$i" -o run \
       --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline --no-check "$@" \
       > "$R/gpurun_out/pmc_$TAG/p$i.log" 2>&1

@@ -12,7 +12,7 @@ for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if "modwt" not in k and "fwt" not in k and "cwt" not in k:
+        if "modwt" not in k and "fwt" not in k and "cwt" not in k and "inv_nomem" not in k:
             continue
         k = k.split("(")[0].replace("void ", "")
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
