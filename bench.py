@@ -24,6 +24,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(ROOT, "jwave-pro_amd"), os.path.join(ROOT, "oracle")]
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -44,6 +45,9 @@ def parse():
     ap.add_argument("--arith", choices=["strict", "fma"], default="fma",
                     help="headline arithmetic; the other contract is timed too and reported")
     ap.add_argument("--no-alt", action="store_true", help="skip timing the other arith mode")
+    ap.add_argument("--workload", choices=["modwt", "cwt"], default="modwt",
+                    help="modwt: the headline metric (BASELINE configs[1]); cwt: configs[2]")
+    ap.add_argument("--scales", type=int, default=64, help="cwt: number of log scales 2..1024")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
     return ap.parse_args()
@@ -81,6 +85,89 @@ def cpu_baseline(wname, n, J, threads):
     }
 
 
+def main_cwt(args, dev, rank, world):
+    """BASELINE configs[2]: ContinuousWaveletTransform(Morlet omega0=6).transformFFT, 64 log
+    scales 2..1024, N=2^18, batch 256 per GPU, fs=1, SYMMETRIC padding (N is a power of 2, so
+    no padding occurs).  One step = one jw_cwt_fft call over the batch (all FFT passes)."""
+    import math
+    import oracle as orc
+    from jwave import ContinuousWaveletTransform as CWT, _native
+    B = args.batch if args.batch != 1024 else 256
+    n = args.n if args.n != (1 << 20) else (1 << 18)
+    ns = args.scales
+    fb, fc = 1.0, 6.0 / (2 * math.pi)
+    scales = CWT.generateLogScales(2.0, 1024.0, ns)
+    lib = _native.lib()
+    stream = torch.cuda.current_stream(dev)
+    sptr = ctypes.c_void_p(stream.cuda_stream)
+    x = torch.empty((B, n), dtype=torch.float64, device=dev)
+    out = torch.empty((B, ns, n, 2), dtype=torch.float64, device=dev)
+    _native.check(lib.jw_synth_uniform(ctypes.c_void_p(x.data_ptr()), n, B, 7 + rank * B, sptr))
+    prm = (ctypes.c_double * 2)(fb, fc)
+    sc = np.ascontiguousarray(scales)
+
+    def call():
+        _native.check(lib.jw_cwt_fft(_native.JW_CWT_MORLET, prm, ctypes.c_void_p(x.data_ptr()), n,
+                                     sc.ctypes.data_as(ctypes.c_void_p), ns, 1.0,
+                                     _native.JW_PAD_SYMMETRIC, ctypes.c_void_p(out.data_ptr()), B,
+                                     _native.JW_DEVICE, sptr))
+
+    for _ in range(args.warmup):
+        call()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        call()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        from jwave import distributed as jdist
+        elapsed = jdist.max_over_ranks(elapsed, device=dev)
+    ms = e0.elapsed_time(e1) / args.steps
+    value = world * B * n * args.steps / elapsed / 1e6
+    per_call = (8 + ns * 16) * B * n  # read the signal, write ns complex coefficients
+    res = None
+    if rank == 0 and not args.no_check:
+        x0 = x[0].cpu().numpy()
+        got = out[0].cpu().numpy()
+        got = got[..., 0] + 1j * got[..., 1]
+        ex = orc.cwt_fft(x0, scales, 1.0, "morlet", (fb, fc), 1, exact=True)
+        jw = orc.cwt_fft(x0, scales, 1.0, "morlet", (fb, fc), 1, exact=False)
+        res = {"vs_exact_twiddles": float(np.max(np.abs(got - ex)) / np.max(np.abs(ex))),
+               "vs_jwave_recurrence": float(np.max(np.abs(got - jw)) / np.max(np.abs(jw)))}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        xs = orc.fill_uniform(n, 7)
+        t0 = time.perf_counter()
+        orc.cwt_fft(xs, scales, 1.0, "morlet", (fb, fc), 1)
+        tc = time.perf_counter() - t0
+        cpu = {"value": n / tc / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
+               "sample": f"1 signal x N={n}, {ns} scales, oracle transformFFT (recurrence-twiddle "
+                         f"radix-2 FFT like FastFourierTransform.java), 1 thread: {tc:.2f} s"}
+    if rank == 0:
+        ach = per_call / (ms * 1e-3) / 1e9
+        print(json.dumps({
+            "metric": f"Msamples/s CWT Morlet(omega0=6) transformFFT, {ns} scales, N=2^18",
+            "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (java.util.Random(7+signal).nextDouble()*2-1, generated in HBM)",
+            "config": {"workload": f"ContinuousWaveletTransform(Morlet fb=1 fc=6/2pi) transformFFT,"
+                                   f" {ns} log scales 2..1024, N={n}, batch={B} per GPU "
+                                   f"(BASELINE configs[2])", "batch_per_gpu": B, "n": n},
+            "parity": res,
+            "roofline": {"bound": "hbm", "kernel": "jw_cwt_fft (all passes, one call)",
+                         "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                         "algorithmic_bytes_per_launch": per_call},
+            "cpu_baseline": cpu}), flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -91,6 +178,8 @@ def main():
     if world > 1:
         from jwave import distributed as jdist
         jdist.init_from_env("nccl", device=dev)
+    if args.workload == "cwt":
+        return main_cwt(args, dev, rank, world)
 
     from jwave import MODWTTransform, _native
     from jwave.transforms import wavelets as W

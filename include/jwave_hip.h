@@ -103,6 +103,28 @@ int jw_fwt2d_reverse(const jw_fwt_plan* plan, const double* y, double* x, int ro
                      int lvlM, int lvlN, int batch, int where, void* stream);
 
 /* ======================================================================
+ * CWT  (replaces ContinuousWaveletTransform.transformFFT :183-229 and
+ *       transformFFTParallel :511-565, which compute the same values)
+ * ====================================================================== */
+#define JW_CWT_MORLET 0 /* MorletWavelet(fb, fc): params = {fb, fc} (MorletWavelet.java:66-124) */
+#define JW_CWT_MEXHAT 1 /* MexicanHatWavelet(sigma): params = {sigma} (MexicanHatWavelet.java) */
+/* ContinuousWaveletTransform.PaddingType (ContinuousWaveletTransform.java:74-79) */
+#define JW_PAD_ZERO 0
+#define JW_PAD_SYMMETRIC 1
+#define JW_PAD_PERIODIC 2
+#define JW_PAD_CONSTANT 3
+
+/* coeffs[b][s][t] = IFFT(FFT(pad(x_b)) * conj(psi_hat(omega, scales[s], 0)))[t], t < n,
+ * for batch signals x (batch x n); out_reim: batch x ns x n complex, interleaved (re, im).
+ * scales: host array of ns positive scales (read at call time).  The padded length is
+ * nextPowerOfTwo(n) <= 2^24.  Parameter checks follow the Java constructors:
+ * fb, fc, sigma > 0 ("Bandwidth parameter must be positive", ...), scales > 0
+ * ("Scale must be positive"). */
+int jw_cwt_fft(int wavelet, const double* params, const double* x, long n, const double* scales,
+               int ns, double sampling_rate, int padding, double* out_reim, int batch, int where,
+               void* stream);
+
+/* ======================================================================
  * Synthetic input (bench / tests): java.util.Random(seed0 + b).nextDouble()*2-1 for
  * signal b, generated in HBM with LCG jump-ahead.  Identical to the oracle's stream.
  * ====================================================================== */

@@ -328,6 +328,38 @@ int jw_fwt2d_reverse(const jw_fwt_plan* plan, const double* y, double* x, int ro
 }
 
 // ---------------------------------------------------------------- synthetic input
+// ---------------------------------------------------------------- CWT
+int jw_cwt_fft(int wavelet, const double* params, const double* x, long n, const double* scales,
+               int ns, double sampling_rate, int padding, double* out_reim, int batch, int where,
+               void* stream) {
+  clear_error();
+  if (wavelet != JW_CWT_MORLET && wavelet != JW_CWT_MEXHAT)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "unknown continuous wavelet kind %d", wavelet);
+  if (!params) return fail(JW_ERR_ILLEGAL_ARGUMENT, "wavelet parameters are null");
+  if (wavelet == JW_CWT_MORLET) {  // MorletWavelet.java:69-74
+    if (!(params[0] > 0)) return fail(JW_ERR_ILLEGAL_ARGUMENT, "Bandwidth parameter must be positive");
+    if (!(params[1] > 0)) return fail(JW_ERR_ILLEGAL_ARGUMENT, "Center frequency must be positive");
+  } else if (!(params[0] > 0)) {  // MexicanHatWavelet.java:67-69
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "Width parameter sigma must be positive");
+  }
+  if (n < 0 || ns < 0 || batch < 0)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "negative size (n=%ld, ns=%d, batch=%d)", n, ns, batch);
+  if (padding < JW_PAD_ZERO || padding > JW_PAD_CONSTANT)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "unknown padding type %d", padding);
+  if (n > 0 && ns > 0 && !scales) return fail(JW_ERR_ILLEGAL_ARGUMENT, "scales are null");
+  for (int i = 0; i < ns && n > 0; ++i)  // ContinuousWavelet.fourierTransform :123-125
+    if (!(scales[i] > 0)) return fail(JW_ERR_ILLEGAL_ARGUMENT, "Scale must be positive");
+  int st = check_where(where);
+  if (st != JW_OK) return st;
+  if (n == 0 || ns == 0 || batch == 0) return JW_OK;
+  const size_t nin = (size_t)batch * n, nout = (size_t)batch * ns * n * 2;
+  return run(where, stream, x, nin, out_reim, nout,
+             [&](const double* xi, double* o, hipStream_t s) {
+               return cwt_fft_device(wavelet, params, xi, n, scales, ns, sampling_rate, padding,
+                                     o, batch, s);
+             });
+}
+
 int jw_synth_uniform(double* x_dev, long n, int batch, long seed0, void* stream) {
   clear_error();
   if (n < 0 || batch < 0) return fail(JW_ERR_ILLEGAL_ARGUMENT, "negative size");

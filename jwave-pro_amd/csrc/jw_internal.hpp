@@ -55,6 +55,9 @@ int modwt_forward_device(const ModwtPlan& p, const double* x, double* coeffs, lo
                          int batch, hipStream_t s);
 int modwt_inverse_device(const ModwtPlan& p, const double* coeffs, double* x, long n, int J,
                          int batch, hipStream_t s);
+int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
+                   const double* scales_host, int ns, double fs, int padding, double* out,
+                   int batch, hipStream_t s);
 int fwt_forward_device(const FwtPlan& p, const double* x, double* y, long n, int level, int batch,
                        hipStream_t s);
 int fwt_reverse_device(const FwtPlan& p, const double* y, double* x, long n, int level, int batch,

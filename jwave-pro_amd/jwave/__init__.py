@@ -6,9 +6,9 @@ All compute goes through libjwave_hip.so (include/jwave_hip.h); there is no CPU 
 """
 from . import exceptions, transforms
 from .Transform import Transform
-from .transforms import FastWaveletTransform, MODWTTransform
+from .transforms import ContinuousWaveletTransform, FastWaveletTransform, MODWTTransform
 from .transforms import wavelets
 
 __version__ = "0.1.0"
-__all__ = ["Transform", "FastWaveletTransform", "MODWTTransform", "wavelets", "exceptions",
-           "transforms"]
+__all__ = ["Transform", "FastWaveletTransform", "MODWTTransform", "ContinuousWaveletTransform",
+           "wavelets", "exceptions", "transforms"]

@@ -21,6 +21,13 @@ JW_ERR_UNSUPPORTED = -5
 JW_HOST = 0
 JW_DEVICE = 1
 
+JW_CWT_MORLET = 0
+JW_CWT_MEXHAT = 1
+JW_PAD_ZERO = 0
+JW_PAD_SYMMETRIC = 1
+JW_PAD_PERIODIC = 2
+JW_PAD_CONSTANT = 3
+
 JW_CONV_AUTO = 0
 JW_CONV_DIRECT = 1
 JW_CONV_FFT = 2
@@ -38,7 +45,7 @@ EXPORTS = (
     "jw_modwt_forward", "jw_modwt_inverse",
     "jw_fwt_plan_create", "jw_fwt_plan_destroy", "jw_fwt_forward", "jw_fwt_reverse",
     "jw_fwt2d_forward", "jw_fwt2d_reverse",
-    "jw_synth_uniform",
+    "jw_synth_uniform", "jw_cwt_fft",
 )
 
 _lib = None
@@ -82,6 +89,7 @@ def lib():
     L.jw_fwt2d_forward.argtypes = [c_dp, c_dp, c_dp, i, i, i, i, i, i, c_dp]
     L.jw_fwt2d_reverse.argtypes = [c_dp, c_dp, c_dp, i, i, i, i, i, i, c_dp]
     L.jw_synth_uniform.argtypes = [c_dp, l, i, l, c_dp]
+    L.jw_cwt_fft.argtypes = [i, c_dp, c_dp, l, c_dp, i, ctypes.c_double, i, c_dp, i, i, c_dp]
     non_int = ("jw_last_error", "jw_version", "jw_modwt_plan_destroy", "jw_fwt_plan_destroy")
     for name in EXPORTS:
         if name not in non_int:

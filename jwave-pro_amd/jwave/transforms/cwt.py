@@ -1,0 +1,167 @@
+"""CWT host mirror: jwave.transforms.ContinuousWaveletTransform on the MI355X.
+
+transformFFT / transformFFTParallel (src/main/java/jwave/transforms/
+ContinuousWaveletTransform.java:183-229, :511-565) run in the HIP engine (jw_cwt_fft): one
+FFT per signal, one pointwise product and IFFT per scale.  Extension beyond the Java API:
+``transformFFTBatch`` takes B x n signals (numpy, or HIP-device torch tensors computed in
+place) and returns B x ns x n complex coefficients.
+"""
+import ctypes
+import enum
+import math
+
+import numpy as np
+
+from .. import _native
+from .._arrays import as_input
+from ..exceptions import IllegalArgumentException
+
+
+class PaddingType(enum.IntEnum):  # ContinuousWaveletTransform.java:74-79
+    ZERO = _native.JW_PAD_ZERO
+    SYMMETRIC = _native.JW_PAD_SYMMETRIC
+    PERIODIC = _native.JW_PAD_PERIODIC
+    CONSTANT = _native.JW_PAD_CONSTANT
+
+
+class CWTResult:
+    """jwave.transforms.CWTResult (CWTResult.java:33-287); coefficients as complex128."""
+
+    def __init__(self, coefficients, scales, timeAxis, samplingRate, waveletName):
+        self._c = coefficients
+        self._scales = np.asarray(scales, dtype=np.float64)
+        self._time = timeAxis
+        self._fs = samplingRate
+        self._name = waveletName
+
+    def getCoefficients(self):
+        return self._c
+
+    def getMagnitude(self):  # Complex.getMag :202-204
+        return np.sqrt(self._c.real * self._c.real + self._c.imag * self._c.imag)
+
+    def getPhase(self):  # Complex.getPhi :213-226 (degrees, quadrant rules) -> radians
+        r, j = self._c.real, self._c.imag
+        with np.errstate(divide="ignore", invalid="ignore"):
+            phi = np.degrees(np.arctan(np.abs(j / r)))
+        out = np.where(r >= 0, np.where(j >= 0, phi, 360.0 - phi),
+                       np.where(j >= 0, 180.0 - phi, phi + 180.0))
+        out = np.where((r == 0) & (j == 0), 0.0, out)
+        return out * math.pi / 180.0
+
+    def getReal(self):
+        return self._c.real.copy()
+
+    def getImaginary(self):
+        return self._c.imag.copy()
+
+    def getScales(self):
+        return self._scales
+
+    def getTimeAxis(self):
+        return self._time
+
+    def scaleToFrequency(self, centerFreq):
+        return centerFreq * self._fs / self._scales
+
+    def getCoefficientsAtScale(self, scaleIndex):
+        if scaleIndex < 0 or scaleIndex >= self._c.shape[0]:
+            raise IndexError("Scale index out of bounds")
+        return self._c[scaleIndex]
+
+    def getCoefficientsAtTime(self, timeIndex):
+        if timeIndex < 0 or timeIndex >= self._c.shape[1]:
+            raise IndexError("Time index out of bounds")
+        return self._c[:, timeIndex].copy()
+
+    def getSamplingRate(self):
+        return self._fs
+
+    def getWaveletName(self):
+        return self._name
+
+    def getNumberOfScales(self):
+        return len(self._scales)
+
+    def getNumberOfTimePoints(self):
+        return len(self._time)
+
+    def getScalogram(self):  # sum_t |c|^2 per scale (CWTResult.java:272-287)
+        m = self.getMagnitude()
+        return np.array([float(np.sum(row * row)) for row in m])
+
+
+class ContinuousWaveletTransform:
+    """jwave.transforms.ContinuousWaveletTransform (FFT path on the GPU)."""
+
+    PaddingType = PaddingType
+
+    def __init__(self, wavelet, paddingType=PaddingType.SYMMETRIC):
+        self._wavelet = wavelet
+        self._paddingType = PaddingType(paddingType)
+        self._name = "Continuous Wavelet Transform"
+
+    def getContinuousWavelet(self):
+        return self._wavelet
+
+    def getName(self):
+        return self._name
+
+    # ---- scale generators (ContinuousWaveletTransform.java:355-405) ----
+    @staticmethod
+    def generateLogScales(minScale, maxScale, numScales):
+        if minScale <= 0 or maxScale <= 0:
+            raise IllegalArgumentException("Scales must be positive")
+        if minScale >= maxScale:
+            raise IllegalArgumentException("minScale must be less than maxScale")
+        if numScales < 2:
+            raise IllegalArgumentException("Need at least 2 scales")
+        lo, hi = math.log(minScale), math.log(maxScale)
+        step = (hi - lo) / (numScales - 1)
+        return np.array([math.exp(lo + i * step) for i in range(numScales)])
+
+    @staticmethod
+    def generateLinearScales(minScale, maxScale, numScales):
+        if minScale <= 0 or maxScale <= 0:
+            raise IllegalArgumentException("Scales must be positive")
+        if minScale >= maxScale:
+            raise IllegalArgumentException("minScale must be less than maxScale")
+        if numScales < 2:
+            raise IllegalArgumentException("Need at least 2 scales")
+        step = (maxScale - minScale) / (numScales - 1)
+        return np.array([minScale + i * step for i in range(numScales)])
+
+    # ---- transforms ----
+    def _run(self, x, scales, samplingRate):
+        sc = np.ascontiguousarray(np.asarray(scales, dtype=np.float64).ravel())
+        B, n = x.shape
+        ns = sc.shape[0]
+        out = x.empty((B, ns, n, 2))
+        params = (ctypes.c_double * 2)(*self._wavelet.params())
+        _native.check(_native.lib().jw_cwt_fft(
+            self._wavelet._kind, params, x.ptr, n, sc.ctypes.data_as(ctypes.c_void_p), ns,
+            float(samplingRate), int(self._paddingType), out.ptr, B, x.where, x.stream))
+        return out
+
+    def transformFFT(self, signal, scales, samplingRate=1.0):
+        x = as_input(np.asarray(signal, dtype=np.float64).reshape(1, -1))
+        out = self._run(x, scales, samplingRate).obj
+        coeffs = out[0, ..., 0] + 1j * out[0, ..., 1]
+        n = coeffs.shape[1]
+        dt = 1.0 / samplingRate
+        time_axis = np.array([i * dt for i in range(n)])  # createTimeAxis
+        return CWTResult(coeffs, scales, time_axis, samplingRate, self._wavelet.getName())
+
+    transformFFTParallel = transformFFT  # same values (ContinuousWaveletTransform.java:511-565)
+
+    def transformFFTBatch(self, signals, scales, samplingRate=1.0):
+        """B x n signals -> B x ns x n complex coefficients (numpy or device torch)."""
+        x = as_input(signals)
+        if len(x.shape) == 1:
+            x = as_input(x.obj.reshape(1, -1))
+        out = self._run(x, scales, samplingRate)
+        if out.device:
+            import torch
+            return torch.view_as_complex(out.obj)
+        o = out.obj
+        return o[..., 0] + 1j * o[..., 1]

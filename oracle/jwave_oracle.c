@@ -218,6 +218,12 @@ void jwo_modwt_inverse_direct(const double* coeffs, long N, int J, const double*
 /* FFT: FastFourierTransform.java forward/reverse :112-164, fftCooleyTukey :172-212,   */
 /* fftCooleyTukeyInternal (no 1/n), fftBluestein :259-324.  Complex.mul :286-288.      */
 /* ------------------------------------------------------------------------ */
+/* Test switch: 1 = correctly rounded twiddles (cosl/sinl per butterfly index) instead of the
+ * reference's recurrence wn = wn * w.  The GPU engine uses exact tables; comparing it with
+ * both variants separates engine error from the reference's own twiddle drift. */
+static int g_exact_twiddles = 0;
+void jwo_set_exact_twiddles(int on) { g_exact_twiddles = on; }
+
 static void fft_ct(double* x, long n, int inverse, int normalize) {
   int p = 0;
   while ((1L << p) < n) p++;
@@ -237,6 +243,12 @@ static void fft_ct(double* x, long n, int inverse, int normalize) {
     for (long start = 0; start < n; start += size) {
       double nr = 1, ni = 0; /* wn = (1,0) */
       for (long k = 0; k < half; k++) {
+        if (g_exact_twiddles) {
+          const long double a = (long double)2 * 3.141592653589793238462643383279503L *
+                                (long double)k / (long double)size * (inverse ? 1 : -1);
+          nr = (double)cosl(a);
+          ni = (double)sinl(a);
+        }
         double* u = x + 2 * (start + k);
         double* v = x + 2 * (start + k + half);
         double ur = u[0], ui = u[1];

@@ -138,13 +138,19 @@ def fwt2d_reverse(y, lvlM, lvlN, wavelet):
     return x
 
 
-def cwt_fft(x, scales, fs=1.0, wavelet="morlet", params=(1.0, 1.0), padding=1):
+def cwt_fft(x, scales, fs=1.0, wavelet="morlet", params=(1.0, 1.0), padding=1, exact=False):
+    """transformFFT restated; exact=True swaps the reference's recurrence twiddles for
+    correctly rounded ones (the engine's choice) -- see jwo_set_exact_twiddles."""
     x, sc = _f64(x), _f64(scales)
     pr = _f64(params)
     n, ns = x.shape[0], sc.shape[0]
     out = np.empty((ns, n, 2))
-    lib().jwo_cwt_fft(0 if wavelet == "morlet" else 1, _p(pr), _p(x), ctypes.c_long(n), _p(sc),
-                      ns, ctypes.c_double(fs), padding, _p(out))
+    lib().jwo_set_exact_twiddles(1 if exact else 0)
+    try:
+        lib().jwo_cwt_fft(0 if wavelet == "morlet" else 1, _p(pr), _p(x), ctypes.c_long(n),
+                          _p(sc), ns, ctypes.c_double(fs), padding, _p(out))
+    finally:
+        lib().jwo_set_exact_twiddles(0)
     return out[..., 0] + 1j * out[..., 1]
 
 

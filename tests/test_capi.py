@@ -141,3 +141,65 @@ def test_raw_capi_rejects_bad_arguments():
                               16, 2, 1, 1, 7, None)
     assert st == _native.JW_ERR_ILLEGAL_ARGUMENT and "where" in _native.last_error()
     lib.jw_modwt_plan_destroy(plan)
+
+
+# ---------------------------------------------------------------- CWT (validation only)
+def test_cwt_wavelet_constructor_messages():
+    from jwave.transforms.wavelets.continuous import MexicanHatWavelet, MorletWavelet
+    with pytest.raises(IllegalArgumentException, match="Bandwidth parameter must be positive"):
+        MorletWavelet(0.0, 1.0)
+    with pytest.raises(IllegalArgumentException, match="Center frequency must be positive"):
+        MorletWavelet(1.0, -1.0)
+    with pytest.raises(IllegalArgumentException, match="Width parameter sigma must be positive"):
+        MexicanHatWavelet(0.0)
+    with pytest.raises(IllegalArgumentException, match="Scale must be positive"):
+        MorletWavelet().fourierTransform([1.0], 0.0)
+
+
+def test_cwt_scale_generators():
+    # ContinuousWaveletTransform.generateLogScales / generateLinearScales (:355-405)
+    from jwave import ContinuousWaveletTransform as C
+    s = C.generateLogScales(2.0, 1024.0, 64)
+    assert s[0] == 2.0 and abs(s[-1] - 1024.0) < 1e-9 and len(s) == 64
+    assert np.all(np.diff(np.log(s)) > 0)
+    assert list(C.generateLinearScales(1.0, 4.0, 4)) == [1.0, 2.0, 3.0, 4.0]
+    for args, msg in [((0.0, 1.0, 4), "Scales must be positive"),
+                      ((2.0, 1.0, 4), "minScale must be less than maxScale"),
+                      ((1.0, 2.0, 1), "Need at least 2 scales")]:
+        with pytest.raises(IllegalArgumentException, match=msg):
+            C.generateLogScales(*args)
+
+
+def test_cwt_capi_rejects_bad_arguments():
+    L = _native.lib()
+    x = np.zeros(8)
+    sc = np.array([1.0, -2.0])
+    out = np.zeros(2 * 8 * 2)
+    p = (ctypes.c_double * 2)(1.0, 1.0)
+    ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    assert L.jw_cwt_fft(0, p, ptr(x), 8, ptr(sc), 2, 1.0, 1, ptr(out), 1, 0, None) == -1
+    assert "Scale must be positive" in _native.last_error()
+    bad = (ctypes.c_double * 2)(0.0, 1.0)
+    assert L.jw_cwt_fft(0, bad, ptr(x), 8, ptr(sc[:1]), 1, 1.0, 1, ptr(out), 1, 0, None) == -1
+    assert "Bandwidth parameter must be positive" in _native.last_error()
+    assert L.jw_cwt_fft(7, p, ptr(x), 8, ptr(sc[:1]), 1, 1.0, 1, ptr(out), 1, 0, None) == -1
+    assert L.jw_cwt_fft(0, p, ptr(x), 8, ptr(sc[:1]), 1, 1.0, 9, ptr(out), 1, 0, None) == -1
+    assert "padding" in _native.last_error()
+    # empty input is a no-op (no device work)
+    assert L.jw_cwt_fft(0, p, ptr(x), 0, ptr(sc[:1]), 1, 1.0, 1, ptr(out), 1, 0, None) == 0
+
+
+def test_cwt_result_accessors():
+    from jwave.transforms import CWTResult
+    c = np.array([[1 + 1j, -1 + 0j, 0j, -2 - 2j], [3 - 4j, 0 + 2j, -1 + 1e-300j, 1 - 1j]])
+    r = CWTResult(c, [1.0, 2.0], np.arange(4.0), 2.0, "Morlet")
+    assert np.allclose(r.getMagnitude()[1, 0], 5.0)
+    ph = r.getPhase()  # Complex.getPhi quadrant rules, radians in [0, 2 pi)
+    assert np.isclose(ph[0, 0], np.pi / 4) and np.isclose(ph[0, 1], np.pi)
+    assert ph[0, 2] == 0.0 and np.isclose(ph[0, 3], 5 * np.pi / 4)
+    assert np.isclose(ph[1, 3], 7 * np.pi / 4)
+    assert list(r.scaleToFrequency(1.0)) == [2.0, 1.0]
+    assert np.allclose(r.getScalogram(), (np.abs(c) ** 2).sum(axis=1))
+    assert r.getNumberOfScales() == 2 and r.getNumberOfTimePoints() == 4
+    with pytest.raises(IndexError):
+        r.getCoefficientsAtScale(2)

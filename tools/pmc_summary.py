@@ -12,9 +12,9 @@ for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if "modwt" not in k and "fwt" not in k and "cwt" not in k and "inv_nomem" not in k:
+        if not any(s in k for s in ("modwt", "fwt", "cwt", "inv_nomem", "pass512", "pass_generic", "psi_table")):
             continue
-        k = k.split("(")[0].replace("void ", "")
+        k = k.replace("(anonymous namespace)", "anon").split("(")[0].replace("void ", "")[:90]
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, v in agg.items():
         for c, x in v.items():
