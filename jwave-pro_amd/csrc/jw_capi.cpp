@@ -147,12 +147,13 @@ int jw_modwt_plan_filters(const jw_modwt_plan* plan, double* g, double* h) {
 }
 
 static int modwt_method_check(int method) {
-  if (method == JW_CONV_AUTO || method == JW_CONV_DIRECT) return JW_OK;
-  if (method == JW_CONV_FFT)
-    return fail(JW_ERR_UNSUPPORTED,
-                "MODWT convolution method FFT is not implemented on the device yet");
+  if (method == JW_CONV_AUTO || method == JW_CONV_DIRECT || method == JW_CONV_FFT) return JW_OK;
   return fail(JW_ERR_ILLEGAL_ARGUMENT, "unknown convolution method %d", method);
 }
+
+// FFT runs the spectral pyramid (jw_modwt_fft.hip) for power-of-two n; AUTO and DIRECT, and
+// FFT at other n, run the direct kernels (exact; within the FFT path's tolerance of it).
+static bool use_fft(int method, long n) { return method == JW_CONV_FFT && modwt_fft_supported(n); }
 
 int jw_modwt_forward(const jw_modwt_plan* plan, const double* x, double* coeffs, long n,
                      int levels, int batch, int method, int where, void* stream) {
@@ -184,7 +185,9 @@ int jw_modwt_forward(const jw_modwt_plan* plan, const double* x, double* coeffs,
   const size_t nin = (size_t)n * batch, nout = (size_t)n * batch * (levels + 1);
   return run(where, stream, x, nin, coeffs, nout,
              [&](const double* dx, double* dc, hipStream_t s) {
-               return modwt_forward_device(*plan, dx, dc, n, levels, batch, s);
+               return use_fft(method, n)
+                          ? modwt_forward_fft_device(*plan, dx, dc, n, levels, batch, s)
+                          : modwt_forward_device(*plan, dx, dc, n, levels, batch, s);
              });
 }
 
@@ -208,7 +211,9 @@ int jw_modwt_inverse(const jw_modwt_plan* plan, const double* coeffs, double* x,
   const size_t nin = (size_t)n * batch * (levels + 1), nout = (size_t)n * batch;
   return run(where, stream, coeffs, nin, x, nout,
              [&](const double* dc, double* dx, hipStream_t s) {
-               return modwt_inverse_device(*plan, dc, dx, n, levels, batch, s);
+               return use_fft(method, n)
+                          ? modwt_inverse_fft_device(*plan, dc, dx, n, levels, batch, s)
+                          : modwt_inverse_device(*plan, dc, dx, n, levels, batch, s);
              });
 }
 

@@ -15,20 +15,22 @@
 #include <algorithm>
 #include <cstdlib>
 
-#include "jw_fft.hpp"
+#include "jw_fft_passes.hpp"
 
 namespace jw {
 namespace {
 
 using fft::cplx;
 using fft::Tables;
+using fft::ColOut;
+using fft::RowIn;
+using fft::SpecOut;
+using fft::SpecOut1;
+using fft::nt_store;
+using fft::run_fft;
+using fft::tpos;
 
 constexpr double kPi = 3.14159265358979323846;  // Math.PI
-typedef double nt2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void nt_store(cplx* p, cplx v) {
-  nt2 w = {v.x, v.y};
-  __builtin_nontemporal_store(w, (nt2*)p);
-}
 
 struct WaveletFT {
   int kind;        // JW_CWT_MORLET / JW_CWT_MEXHAT
@@ -53,108 +55,10 @@ __device__ __forceinline__ double psi_hat(const WaveletFT& w, double omega, doub
   return v * sqrt_scale;  // ft.mul(Math.sqrt(scale))
 }
 
-// ---------------------------------------------------------------------------------------
-// Pass kernels.  Pass 1 ("columns"): item, column col < N2; inputs k = N2*k1 + col, k1 < N1;
-// outputs n1 < N1, multiplied by W_N^(S n1 col) when N2 > 1.  Pass 2 ("rows"): item, row n1;
-// inputs k2 < N2 of that row; outputs n2 < N2.  In/Out are functors:
-//   cplx in(long item, long idx_in_line, long line)     (idx = k1 or k2, line = col or n1)
-//   void out(long item, long idx_out, long line, cplx v)
-// Fast kernels: 512-point lines, 8 lines per workgroup, one per wavefront, staged through a
-// padded LDS tile so global reads/writes move 8 consecutive complex values (128 bytes).
-// ---------------------------------------------------------------------------------------
-constexpr int kT = 8;                  // lines per workgroup (fast kernels)
-constexpr int kTile = 512 * (kT + 1);  // padded tile, also holds the 8 exchange buffers
-static_assert(kTile >= kT * fft::kXbuf, "tile must hold the exchange buffers");
-
-// IN_TILE: the line's inputs are strided (pass 1 over a natural-order array): stage 8 lines
-// through the tile.  TWID: apply the four-step twiddle W_N^(S n1 col) (pass 1).
-template <int S, bool IN_TILE, bool TWID, class In, class Out>
-__global__ __launch_bounds__(512) void pass512(In in, Out out, long N, long N2, Tables T) {
-  __shared__ cplx tile[kTile];
-  const int tid = threadIdx.x, lane = tid & 63, c = tid >> 6;
-  const long item = blockIdx.y;
-  const long line0 = (long)blockIdx.x * kT;
-  cplx a[8];
-  if (IN_TILE) {
-    // tile[k1][c] <- in(k1, line0 + c): 8 consecutive columns per row, coalesced
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int k1 = (tid >> 3) + 64 * i, cc = tid & 7;
-      tile[k1 * (kT + 1) + cc] = in(item, k1, line0 + cc);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 8; ++r) a[r] = tile[(lane + 64 * r) * (kT + 1) + c];
-    __syncthreads();
-  } else {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) a[r] = in(item, lane + 64 * r, line0 + c);
-  }
-  fft::fft512_wave<S>(a, tile + c * fft::kXbuf, T.w512, lane);
-  const int q = lane >> 3, k1 = lane & 7;
-  if (TWID && N2 > 1) {
-    // W_N^(n1 col) for n1 = q + 8 k1 + 64 k2: one table lookup per lane, then the
-    // wave-uniform step W_N^(64 col) applied k2 times (7 products: ~1e-15 relative)
-    const long col = line0 + c;
-    cplx w = fft::twiddle(T, ((long)(q + 8 * k1) * col) & (N - 1));
-    const cplx step = fft::twiddle(T, (64 * col) & (N - 1));
-#pragma unroll
-    for (int k2 = 0; k2 < 8; ++k2) {
-      a[k2] = fft::cmul_tw<S>(a[k2], w);
-      if (k2 < 7) w = fft::cmul(w, step);
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k2 = 0; k2 < 8; ++k2) tile[(q + 8 * k1 + 64 * k2) * (kT + 1) + c] = a[k2];
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int n = (tid >> 3) + 64 * i, cc = tid & 7;
-    out(item, n, line0 + cc, tile[n * (kT + 1) + cc]);
-  }
-}
-
-// Generic line FFT of M = 2^logM <= 4096 points, one workgroup per line: bit-reversed load,
-// in-place radix-2 stages in LDS.
-template <int S, bool COLS, class In, class Out>
-__global__ __launch_bounds__(256) void pass_generic(In in, Out out, long N, long N2, int logM,
-                                                    Tables T) {
-  extern __shared__ cplx buf[];
-  const int tid = threadIdx.x;
-  const int M = 1 << logM;
-  const long item = blockIdx.y, line = blockIdx.x;
-  for (int j = tid; j < M; j += 256) {
-    const int r = logM ? (int)(__brev((unsigned)j) >> (32 - logM)) : 0;
-    buf[r] = in(item, j, line);
-  }
-  __syncthreads();
-  for (int len = 2; len <= M; len <<= 1) {
-    const int half = len >> 1;
-    const long step = N / len;
-    for (int b = tid; b < (M >> 1); b += 256) {
-      const int pos = b & (half - 1);
-      const int i0 = (b - pos) * 2 + pos, i1 = i0 + half;
-      const cplx w = fft::twiddle(T, pos * step);
-      const cplx u = buf[i0], v = fft::cmul_tw<S>(buf[i1], w);
-      buf[i0] = fft::cadd(u, v);
-      buf[i1] = fft::csub(u, v);
-    }
-    __syncthreads();
-  }
-  for (int j = tid; j < M; j += 256) {
-    cplx v = buf[j];
-    if (COLS && N2 > 1) v = fft::cmul_tw<S>(v, fft::twiddle(T, ((long)j * line) & (N - 1)));
-    out(item, j, line, v);
-  }
-}
 
 // ---------------------------------------------------------------------------------------
 // Functors
 // ---------------------------------------------------------------------------------------
-// Spectra are stored "column-major" for the inverse's four-step: element k at
-// (k mod N2) * N1 + k / N2, so each pass-1 column is contiguous.
-__device__ __forceinline__ long tpos(long k, long N1, long N2) { return (k % N2) * N1 + k / N2; }
 
 struct PadIn {  // padded real signal, element k (padSignal :269-306)
   static constexpr bool kStrided = true;
@@ -176,40 +80,6 @@ struct PadIn {  // padded real signal, element k (padSignal :269-306)
       v = xs[n - 1];
     }
     return make_double2(v, 0.0);
-  }
-};
-struct RowIn {  // A[item][n1 * N2 + k2]
-  const cplx* A;
-  long N, N2;
-  __device__ cplx operator()(long item, long k2, long n1) const {
-    return A[item * N + n1 * N2 + k2];
-  }
-};
-struct ColOut {  // A[item][n1 * N2 + col]
-  cplx* A;
-  long N, N2;
-  bool nt;  // non-temporal stores
-  __device__ void operator()(long item, long n1, long col, cplx v) const {
-    if (nt) {  // streamed once: keep it from evicting the spectra out of L2
-      nt_store(&A[item * N + n1 * N2 + col], v);
-    } else {
-      A[item * N + n1 * N2 + col] = v;
-    }
-  }
-};
-struct SpecOut {  // X[item][k], k = n1 + N1 * n2, at its column-major position
-  cplx* X;
-  long N, N1, N2;
-  long item0;
-  __device__ void operator()(long item, long idx, long line, cplx v) const {
-    X[(item0 + item) * N + tpos(line + N1 * idx, N1, N2)] = v;
-  }
-};
-struct SpecOut1 {  // single pass: X[item][idx]
-  cplx* X;
-  long N, item0;
-  __device__ void operator()(long item, long idx, long, cplx v) const {
-    X[(item0 + item) * N + idx] = v;
   }
 };
 struct ScaleIn {  // X[sig][k] * psi_hat(omega_k, a_s), k = N2 k1 + col; item = pair in group
@@ -252,42 +122,6 @@ struct CoefOut {  // out[pair][t] = v / N for t = line + N1 * idx < n  (reverse 
   }
 };
 
-// One full FFT (forward or reverse) of `items` lines of length N: in(item, k) -> out.
-template <int S, class In1, class Out1, class Out2>
-int run_fft(long N, long items, In1 in1, Out1 out_single, Out2 out_final, cplx* A, hipStream_t s,
-            const Tables& T, bool a_nt) {
-  int logN = 0;
-  while ((1L << logN) < N) ++logN;
-  if (N <= 4096) {  // one pass, N2 = 1
-    hipLaunchKernelGGL((pass_generic<S, true, In1, Out1>), dim3(1, (unsigned)items), dim3(256),
-                       (size_t)N * sizeof(cplx), s, in1, out_single, N, 1L, logN, T);
-    JW_HIP_TRY(hipGetLastError());
-    return JW_OK;
-  }
-  const int log1 = (logN + 1) / 2, log2 = logN - log1;
-  const long N1 = 1L << log1, N2 = 1L << log2;
-  ColOut a_out{A, N, N2, a_nt};
-  RowIn a_in{A, N, N2};
-  if (N1 == 512) {
-    hipLaunchKernelGGL((pass512<S, In1::kStrided, true, In1, ColOut>),
-                       dim3((unsigned)(N2 / kT), (unsigned)items), dim3(512), 0, s, in1, a_out, N,
-                       N2, T);
-  } else {
-    hipLaunchKernelGGL((pass_generic<S, true, In1, ColOut>), dim3((unsigned)N2, (unsigned)items),
-                       dim3(256), (size_t)N1 * sizeof(cplx), s, in1, a_out, N, N2, log1, T);
-  }
-  JW_HIP_TRY(hipGetLastError());
-  if (N2 == 512) {
-    hipLaunchKernelGGL((pass512<S, false, false, RowIn, Out2>),
-                       dim3((unsigned)(N1 / kT), (unsigned)items), dim3(512), 0, s, a_in, out_final,
-                       N, N2, T);
-  } else {
-    hipLaunchKernelGGL((pass_generic<S, false, RowIn, Out2>), dim3((unsigned)N1, (unsigned)items),
-                       dim3(256), (size_t)N2 * sizeof(cplx), s, a_in, out_final, N, N2, log2, T);
-  }
-  JW_HIP_TRY(hipGetLastError());
-  return JW_OK;
-}
 
 }  // namespace
 

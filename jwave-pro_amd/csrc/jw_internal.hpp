@@ -55,6 +55,11 @@ int modwt_forward_device(const ModwtPlan& p, const double* x, double* coeffs, lo
                          int batch, hipStream_t s);
 int modwt_inverse_device(const ModwtPlan& p, const double* coeffs, double* x, long n, int J,
                          int batch, hipStream_t s);
+bool modwt_fft_supported(long n);
+int modwt_forward_fft_device(const ModwtPlan& p, const double* x, double* coeffs, long n, int J,
+                             int batch, hipStream_t s);
+int modwt_inverse_fft_device(const ModwtPlan& p, const double* coeffs, double* x, long n, int J,
+                             int batch, hipStream_t s);
 int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
                    const double* scales_host, int ns, double fs, int padding, double* out,
                    int batch, hipStream_t s);
