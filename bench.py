@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--arith", choices=["strict", "fma"], default="fma",
                     help="headline arithmetic; the other contract is timed too and reported")
     ap.add_argument("--no-alt", action="store_true", help="skip timing the other arith mode")
-    ap.add_argument("--workload", choices=["modwt", "cwt"], default="modwt",
+    ap.add_argument("--workload", choices=["modwt", "cwt", "fwt2d"], default="modwt",
                     help="modwt: the headline metric (BASELINE configs[1]); cwt: configs[2]")
     ap.add_argument("--scales", type=int, default=64, help="cwt: number of log scales 2..1024")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -168,6 +168,95 @@ def main_cwt(args, dev, rank, world):
             "cpu_baseline": cpu}), flush=True)
 
 
+def main_fwt2d(args, dev, rank, world):
+    """BASELINE configs[3]: FastWaveletTransform(Daubechies8) 2-D forward + reverse on 4096 x
+    4096 images, batch 64 per GPU, full levels (getExponent = 12 per axis).  One step = one
+    jw_fwt2d_forward + one jw_fwt2d_reverse over the batch."""
+    import oracle as orc
+    from jwave import _native
+    from jwave.transforms import wavelets as W
+    B = args.batch if args.batch != 1024 else 64
+    R = 4096
+    lvl = 12
+    wv = W.Daubechies8()
+    lib = _native.lib()
+    stream = torch.cuda.current_stream(dev)
+    sptr = ctypes.c_void_p(stream.cuda_stream)
+    plan = ctypes.c_void_p()
+    arr = lambda v: (ctypes.c_double * len(v))(*v)  # noqa: E731
+    arith = _native.JW_ARITH_FMA if args.arith == "fma" else _native.JW_ARITH_STRICT
+    _native.check(lib.jw_fwt_plan_create(
+        ctypes.byref(plan), arr(wv.getScalingDeComposition()), arr(wv.getWaveletDeComposition()),
+        arr(wv.getScalingReConstruction()), arr(wv.getWaveletReConstruction()),
+        wv.getMotherWavelength(), wv.getTransformWavelength(), getattr(wv, "kind", 0), arith))
+    x = torch.empty((B, R, R), dtype=torch.float64, device=dev)
+    y = torch.empty_like(x)
+    xr = torch.empty_like(x)
+    _native.check(lib.jw_synth_uniform(ctypes.c_void_p(x.data_ptr()), R * R, B, 11 + rank * B,
+                                       sptr))
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+
+    def fwd():
+        _native.check(lib.jw_fwt2d_forward(plan, P(x), P(y), R, R, lvl, lvl, B,
+                                           _native.JW_DEVICE, sptr))
+
+    def rev():
+        _native.check(lib.jw_fwt2d_reverse(plan, P(y), P(xr), R, R, lvl, lvl, B,
+                                           _native.JW_DEVICE, sptr))
+
+    for _ in range(args.warmup):
+        fwd()
+        rev()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    t0 = time.perf_counter()
+    fms = rms_ = 0.0
+    for _ in range(args.steps):
+        ev[0].record(stream)
+        fwd()
+        ev[1].record(stream)
+        rev()
+        ev[2].record(stream)
+        torch.cuda.synchronize()
+        fms += ev[0].elapsed_time(ev[1])
+        rms_ += ev[1].elapsed_time(ev[2])
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        from jwave import distributed as jdist
+        elapsed = jdist.max_over_ranks(elapsed, device=dev)
+    fms /= args.steps
+    rms_ /= args.steps
+    value = world * B * R * R * args.steps / elapsed / 1e6
+    err = ((xr - x).abs().max() / x.abs().max()).item()
+    check = None
+    if rank == 0 and not args.no_check:
+        ref = orc.fwt2d_forward(x[0].cpu().numpy(), lvl, lvl, wv)
+        got = y[0].cpu().numpy()
+        check = "bit-exact" if np.array_equal(ref, got) else \
+            f"normwise {np.max(np.abs(ref - got)) / np.max(np.abs(ref)):.3g}"
+    lib.jw_fwt_plan_destroy(plan)
+    if rank == 0:
+        per = 64 * B * R * R  # 2 passes x (read + write) x 8 B, forward + reverse
+        ach = per / ((fms + rms_) * 1e-3) / 1e9
+        print(json.dumps({
+            "metric": "Mpixels/s FWT Daubechies8 2-D forward+reverse (4096x4096, 12x12 levels)",
+            "value": round(value, 2), "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (java.util.Random(11+image).nextDouble()*2-1, generated in HBM)",
+            "config": {"workload": f"FastWaveletTransform(Daubechies8) 2-D fwd+rev, 4096x4096, "
+                                   f"batch={B} per GPU (BASELINE configs[3])", "arith": args.arith},
+            "max_recon_error": err, "spot_check_vs_oracle": check,
+            "roofline": {"bound": "hbm", "kernel": "jw_fwt2d_forward + jw_fwt2d_reverse",
+                         "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                         "algorithmic_bytes_per_step": per, "fwd_ms": round(fms, 3),
+                         "rev_ms": round(rms_, 3)},
+            "cpu_baseline": None}), flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -180,6 +269,8 @@ def main():
         jdist.init_from_env("nccl", device=dev)
     if args.workload == "cwt":
         return main_cwt(args, dev, rank, world)
+    if args.workload == "fwt2d":
+        return main_fwt2d(args, dev, rank, world)
 
     from jwave import MODWTTransform, _native
     from jwave.transforms import wavelets as W

@@ -110,3 +110,23 @@ def test_haar_orthogonal_integer_exact():
     x = np.arange(-512.0, 512.0)
     y = f.forward(x, 10)
     assert np.all(y == np.round(y)) and bits_equal(f.reverse(y, 10), x)
+
+
+@pytest.mark.parametrize("wname", ["Haar1", "Daubechies2", "Daubechies8", "Symlet20", "Coiflet5",
+                                   "Haar1Orthogonal"])
+def test_fast_and_generic_lds_kernels_agree(wname, monkeypatch):
+    # JW_FWT_GENERIC forces the original LDS kernels; both are bit-identical to the oracle
+    wv = wavelet(wname)
+    f = FastWaveletTransform(wv)
+    for n, lvl in [(4, 2), (32, 5), (4096, 12), (4096, 3)]:
+        x = orc.fill_uniform(n, 17 + n)
+        ref = orc.fwt_forward(x, lvl, wv)
+        y_fast = f.forward(x, lvl)
+        r_fast = f.reverse(ref, lvl)
+        monkeypatch.setenv("JW_FWT_GENERIC", "1")
+        y_gen = f.forward(x, lvl)
+        r_gen = f.reverse(ref, lvl)
+        monkeypatch.delenv("JW_FWT_GENERIC")
+        rref = orc.fwt_reverse(ref, lvl, wv)
+        assert bits_equal(y_fast, ref) and bits_equal(y_gen, ref), (n, lvl)
+        assert bits_equal(r_fast, rref) and bits_equal(r_gen, rref), (n, lvl)
