@@ -78,28 +78,25 @@ int main() {
   hipMemset(c, 0, 9L * N * B * 8);
   Taps taps{};
   for (int m = 0; m < 8; ++m) { taps.a[m] = 0.1 * m; taps.b[m] = 0.2 - 0.01 * m; }
-  using G = GeoI<8, 8, 256>;
-  const size_t lds = (size_t)G::inv_total * 8;
-  const long steps = 131072 / 256 + 8;  // as the real kernel at cfg2 (segment + warm-up)
-  auto time = [&](auto kern, const char* name) {
+  auto time = [&](auto kern, int C, const char* name) {
+    const size_t lds = (size_t)(2 * (Geo<8, 8>::H + 8 * C)) * 8;
+    const long steps = 131072 / C + (2048 + C - 1) / C;  // segment + warm-up, as at cfg2
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipEvent_t e0, e1;
     hipEventCreate(&e0); hipEventCreate(&e1);
     dim3 g(8, B);
-    kern<<<g, 256, lds>>>(c, x, N, steps, taps);
+    kern<<<g, C, lds>>>(c, x, N, steps, taps);
     hipEventRecord(e0);
-    for (int i = 0; i < 3; ++i) kern<<<g, 256, lds>>>(c, x, N, steps, taps);
+    for (int i = 0; i < 3; ++i) kern<<<g, C, lds>>>(c, x, N, steps, taps);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     float ms; hipEventElapsedTime(&ms, e0, e1);
-    printf("%-28s %8.3f ms\n", name, ms / 3);
+    printf("%-34s %8.3f ms\n", name, ms / 3);
   };
-  time(inv_nomem<8, 8, true, 256, 256, 2, 2>, "fma, loads+stores D2");
-  time(inv_nomem<8, 8, true, 256, 256, 2, 2, 7>, "fma, loads+stores ring7");
-  time(inv_nomem<8, 8, true, 256, 256, 2, false, 7>, "fma, no HBM ring7");
-  time(inv_nomem<8, 8, true, 256, 256, 2, false>, "fma, no HBM");
-  time(inv_nomem<8, 8, false, 256, 256, 2, false>, "strict, no HBM");
-  time(inv_nomem<8, 8, true, 256, 256, 2, true>, "fma, loads only");
+  time(inv_nomem<8, 8, true, 256, 256, 2, 2, 7>, 256, "C256 fma, loads+stores ring7");
+  time(inv_nomem<8, 8, true, 256, 256, 2, false, 7>, 256, "C256 fma, no HBM ring7");
+  time(inv_nomem<8, 8, false, 256, 256, 2, 2, 7>, 256, "C256 strict, loads+stores ring7");
+  time(inv_nomem<8, 8, false, 256, 256, 2, false, 7>, 256, "C256 strict, no HBM ring7");
 
   return 0;
 }
