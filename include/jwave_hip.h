@@ -99,6 +99,12 @@ int jw_fwt_forward(const jw_fwt_plan* plan, const double* x, double* y, long n, 
                    int batch, int where, void* stream);
 int jw_fwt_reverse(const jw_fwt_plan* plan, const double* y, double* x, long n, int level,
                    int batch, int where, void* stream);
+/* WaveletPacketTransform.forward/reverse(double[], level) (WaveletPacketTransform.java:60-191):
+ * every level transforms all n/h packets.  Same plan and arithmetic as the FWT. */
+int jw_wpt_forward(const jw_fwt_plan* plan, const double* x, double* y, long n, int level,
+                   int batch, int where, void* stream);
+int jw_wpt_reverse(const jw_fwt_plan* plan, const double* y, double* x, long n, int level,
+                   int batch, int where, void* stream);
 /* 2-D: rows with lvlN then columns with lvlM (reverse: columns, then rows). */
 int jw_fwt2d_forward(const jw_fwt_plan* plan, const double* x, double* y, int rows, int cols,
                      int lvlM, int lvlN, int batch, int where, void* stream);

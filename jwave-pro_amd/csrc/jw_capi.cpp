@@ -298,6 +298,48 @@ int jw_fwt_reverse(const jw_fwt_plan* plan, const double* y, double* x, long n, 
   });
 }
 
+// WaveletPacketTransform.forward/reverse validation (WaveletPacketTransform.java:63-72, :122-131).
+static int wpt_check(long n, int level, const char* who) {
+  if (!is_binary(n))
+    return fail(JW_ERR_FAILURE,
+                "given array length is not 2^p | p E N ... = 1, 2, 4, 8, 16, 32, .. please use "
+                "the Ancient Egyptian Decomposition for any other array length!");
+  if (level < 0 || level > floor_log2(n))
+    return fail(JW_ERR_FAILURE,
+                "WaveletPacketTransform#%s - given level is out of range for given array", who);
+  return JW_OK;
+}
+
+int jw_wpt_forward(const jw_fwt_plan* plan, const double* x, double* y, long n, int level,
+                   int batch, int where, void* stream) {
+  clear_error();
+  if (!plan) return fail(JW_ERR_ILLEGAL_ARGUMENT, "plan is null");
+  int st = wpt_check(n, level, "forward");
+  if (st != JW_OK) return st;
+  if (st = check_where(where); st != JW_OK) return st;
+  if (batch <= 0) return batch == 0 ? JW_OK : fail(JW_ERR_ILLEGAL_ARGUMENT, "negative batch");
+  if (!x || !y) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
+  const size_t elems = (size_t)n * batch;
+  return run(where, stream, x, elems, y, elems, [&](const double* dx, double* dy, hipStream_t s) {
+    return wpt_forward_device(*plan, dx, dy, n, level, batch, s);
+  });
+}
+
+int jw_wpt_reverse(const jw_fwt_plan* plan, const double* y, double* x, long n, int level,
+                   int batch, int where, void* stream) {
+  clear_error();
+  if (!plan) return fail(JW_ERR_ILLEGAL_ARGUMENT, "plan is null");
+  int st = wpt_check(n, level, "reverse");
+  if (st != JW_OK) return st;
+  if (st = check_where(where); st != JW_OK) return st;
+  if (batch <= 0) return batch == 0 ? JW_OK : fail(JW_ERR_ILLEGAL_ARGUMENT, "negative batch");
+  if (!x || !y) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
+  const size_t elems = (size_t)n * batch;
+  return run(where, stream, y, elems, x, elems, [&](const double* dy, double* dx, hipStream_t s) {
+    return wpt_reverse_device(*plan, dy, dx, n, level, batch, s);
+  });
+}
+
 int jw_fwt2d_forward(const jw_fwt_plan* plan, const double* x, double* y, int rows, int cols,
                      int lvlM, int lvlN, int batch, int where, void* stream) {
   clear_error();

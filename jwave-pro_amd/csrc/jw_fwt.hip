@@ -322,6 +322,137 @@ __global__ __launch_bounds__(kNT2) void fwt_rev_lds2(const double* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------------
+// Wavelet packet transform (WaveletPacketTransform.java:60-191): every level applies
+// Wavelet.forward / reverse to each of the n/h packets of length h, not just the first.
+// Same per-packet arithmetic as the FWT cascades above (bit-identical in STRICT).
+// ---------------------------------------------------------------------------------------
+template <bool FMA, int M>
+__global__ __launch_bounds__(kNT2) void wpt_fwd_lds(const double* __restrict__ x,
+                                                   double* __restrict__ y, int n, int level, int tw,
+                                                   Filters f) {
+  __shared__ __attribute__((aligned(16))) double buf[kLdsN];
+  constexpr int P = kLdsN / kNT2 / 2;
+  const int tid = threadIdx.x;
+  const double* xs = x + (long)blockIdx.x * n;
+  double* ys = y + (long)blockIdx.x * n;
+  for (int i = 2 * tid; i < n; i += 2 * kNT2) *(d2*)&buf[i] = *(const d2*)&xs[i];
+  __syncthreads();
+  const int npairs = n >> 1;
+  int l = 0;
+  for (int h = n; h >= tw && h >= 2 && l < level; h >>= 1, ++l) {
+    const int half = h >> 1, mask = h - 1, lh = 31 - __builtin_clz(half);
+    double lo[P], hi[P];
+#pragma unroll
+    for (int r = 0; r < P; ++r) {
+      const int q = tid + r * kNT2;
+      lo[r] = 0.;
+      hi[r] = 0.;
+      if (q < npairs) {
+        const int base = (q >> lh) * h, i = q & (half - 1);
+#pragma unroll
+        for (int t = 0; t < (M >> 1); ++t) {
+          const d2 v = *(const d2*)&buf[base + ((2 * i + 2 * t) & mask)];
+          lo[r] = madd<FMA>(lo[r], f.sD[2 * t], v.x);
+          hi[r] = madd<FMA>(hi[r], f.wD[2 * t], v.x);
+          lo[r] = madd<FMA>(lo[r], f.sD[2 * t + 1], v.y);
+          hi[r] = madd<FMA>(hi[r], f.wD[2 * t + 1], v.y);
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < P; ++r) {
+      const int q = tid + r * kNT2;
+      if (q < npairs) {
+        const int base = (q >> lh) * h, i = q & (half - 1);
+        buf[base + i] = lo[r];
+        buf[base + i + half] = hi[r];
+      }
+    }
+    __syncthreads();
+  }
+  for (int i = 2 * tid; i < n; i += 2 * kNT2) *(d2*)&ys[i] = *(const d2*)&buf[i];
+}
+
+template <bool FMA, int M, int KIND>
+__global__ __launch_bounds__(kNT2) void wpt_rev_lds(const double* __restrict__ y,
+                                                   double* __restrict__ x, int n, int h0, int tw,
+                                                   Filters f) {
+  __shared__ __attribute__((aligned(16))) double buf[kLdsN];
+  constexpr int P = kLdsN / kNT2 / 2;
+  const int tid = threadIdx.x;
+  const double* ys = y + (long)blockIdx.x * n;
+  double* xs = x + (long)blockIdx.x * n;
+  for (int i = 2 * tid; i < n; i += 2 * kNT2) *(d2*)&buf[i] = *(const d2*)&ys[i];
+  __syncthreads();
+  const int npairs = n >> 1;
+  for (int h = h0; h <= n && h >= tw && h >= 2; h <<= 1) {
+    const int half = h >> 1, lh = 31 - __builtin_clz(half);
+    const int nslow = h < M ? half : (M >> 1) - 1 < half ? (M >> 1) - 1 : half;
+    d2 o[P];
+#pragma unroll
+    for (int r = 0; r < P; ++r) {
+      const int q = tid + r * kNT2;
+      if (q < npairs) {
+        const int base = (q >> lh) * h, u = q & (half - 1);
+        if (u >= nslow) {
+          double a0 = 0., a1 = 0.;
+#pragma unroll
+          for (int t = (M >> 1) - 1; t >= 0; --t) {
+            const double av = buf[base + u - t], dv = buf[base + u - t + half];
+            a0 += contrib<FMA>(av, dv, f.sR[2 * t], f.wR[2 * t], KIND);
+            a1 += contrib<FMA>(av, dv, f.sR[2 * t + 1], f.wR[2 * t + 1], KIND);
+          }
+          o[r] = d2{a0, a1};
+        } else {
+          o[r] = rev_pair_wrapped<FMA, M, KIND>(buf + base, h, u, f);
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < P; ++r) {
+      const int q = tid + r * kNT2;
+      if (q < npairs) {
+        const int base = (q >> lh) * h, u = q & (half - 1);
+        *(d2*)&buf[base + 2 * u] = o[r];
+      }
+    }
+    __syncthreads();
+  }
+  for (int i = 2 * tid; i < n; i += 2 * kNT2) *(d2*)&xs[i] = *(const d2*)&buf[i];
+}
+
+// One WPT level on global memory (any M, any power-of-two n): out-of-place.
+template <bool FMA>
+__global__ __launch_bounds__(kNT) void wpt_fwd_level(const double* __restrict__ in,
+                                                     double* __restrict__ out, long n, int h, int M,
+                                                     Filters f) {
+  const long q = (long)blockIdx.x * kNT + threadIdx.x;
+  if (q >= (n >> 1)) return;
+  const int half = h >> 1;
+  const long base = (q / half) * h;
+  const int i = (int)(q % half);
+  const double* src = in + (long)blockIdx.y * n + base;
+  double* dst = out + (long)blockIdx.y * n + base;
+  double lo, hi;
+  fwd_pair<FMA>(src, h, i, M, f, lo, hi);
+  dst[i] = lo;
+  dst[i + half] = hi;
+}
+
+template <bool FMA>
+__global__ __launch_bounds__(kNT) void wpt_rev_level(const double* __restrict__ in,
+                                                     double* __restrict__ out, long n, int h, int M,
+                                                     int kind, Filters f) {
+  const long k = (long)blockIdx.x * kNT + threadIdx.x;
+  if (k >= n) return;
+  const long base = (k / h) * h;
+  out[(long)blockIdx.y * n + k] =
+      rev_out<FMA>(in + (long)blockIdx.y * n + base, h, (int)(k - base), M, kind, f.sR, f.wR);
+}
+
+// ---------------------------------------------------------------------------------------
 // 2-D passes with the transpose fused in: a workgroup (1024 threads) transforms 4 lines of
 // one matrix at once, one 256-thread group per line.  READ_T: the lines are columns of the
 // [len][nlines] input (read as 4 consecutive doubles per row); WRITE_T: line i is written as
@@ -606,6 +737,95 @@ int fwt_reverse_device(const FwtPlan& p, const double* y, double* x, long n, int
                        hipStream_t s) {
   return p.arith == JW_ARITH_FMA ? reverse_t<true>(p, y, x, n, level, batch, s)
                                  : reverse_t<false>(p, y, x, n, level, batch, s);
+}
+
+namespace {
+
+template <bool FMA>
+bool launch_wpt_lds(bool rev, int M, int kind, dim3 g, hipStream_t s, const double* in,
+                    double* out, int n, int lvl_h0, int tw, const Filters& f) {
+  switch (M) {
+#define JW_C(MM)                                                                                \
+  case MM:                                                                                      \
+    if (!rev)                                                                                   \
+      hipLaunchKernelGGL((wpt_fwd_lds<FMA, MM>), g, dim3(kNT2), 0, s, in, out, n, lvl_h0, tw, f); \
+    else if (kind == JW_WAVELET_HAAR_ORTH)                                                       \
+      hipLaunchKernelGGL((wpt_rev_lds<FMA, MM, JW_WAVELET_HAAR_ORTH>), g, dim3(kNT2), 0, s, in, \
+                         out, n, lvl_h0, tw, f);                                                 \
+    else                                                                                        \
+      hipLaunchKernelGGL((wpt_rev_lds<FMA, MM, JW_WAVELET_GENERIC>), g, dim3(kNT2), 0, s, in,    \
+                         out, n, lvl_h0, tw, f);                                                 \
+    return true;
+    JW_FWT_LENGTHS(JW_C)
+#undef JW_C
+    default:
+      return false;
+  }
+}
+
+template <bool FMA>
+int wpt_t(const FwtPlan& p, bool rev, const double* in, double* out, long n, int level, long batch,
+          hipStream_t s) {
+  const Filters f = make_filters(p);
+  long h0 = p.tw;
+  if (rev)
+    for (int l = level; l < log2_exact(n); ++l) h0 <<= 1;  // WaveletPacketTransform.java:160-162
+  const int lvl_h0 = rev ? (int)h0 : level;
+  if (n <= kLdsN && n >= 2 && p.M % 2 == 0 && !std::getenv("JW_FWT_GENERIC")) {
+    bool ok = true;
+    for (long b0 = 0; b0 < batch && ok; b0 += 1L << 30) {
+      const long nb = batch - b0 < (1L << 30) ? batch - b0 : (1L << 30);
+      ok = launch_wpt_lds<FMA>(rev, p.M, p.kind, dim3((unsigned)nb), s, in + b0 * n, out + b0 * n,
+                               (int)n, lvl_h0, p.tw, f);
+    }
+    if (ok) {
+      JW_HIP_TRY(hipGetLastError());
+      return JW_OK;
+    }
+  }
+  // per-level global kernels, ping-pong between out and a workspace
+  double* tmp = nullptr;
+  JW_HIP_TRY(hipMallocAsync((void**)&tmp, sizeof(double) * (size_t)(n * batch), s));
+  if (out != in) JW_HIP_TRY(hipMemcpyAsync(out, in, sizeof(double) * n * batch, hipMemcpyDeviceToDevice, s));
+  double *a = out, *b = tmp;
+  int l = 0;
+  for (long h = rev ? h0 : n; rev ? (h <= n && h >= p.tw) : (h >= p.tw && l < level);
+       h = rev ? h << 1 : h >> 1, ++l) {
+    if (h < 2) break;
+    for (long b0 = 0; b0 < batch; b0 += 65535) {
+      const long nb = batch - b0 < 65535 ? batch - b0 : 65535;
+      if (rev) {
+        hipLaunchKernelGGL(wpt_rev_level<FMA>, dim3((unsigned)((n + kNT - 1) / kNT), (unsigned)nb),
+                           dim3(kNT), 0, s, a + b0 * n, b + b0 * n, n, (int)h, p.M, p.kind, f);
+      } else {
+        hipLaunchKernelGGL(wpt_fwd_level<FMA>,
+                           dim3((unsigned)(((n >> 1) + kNT - 1) / kNT), (unsigned)nb), dim3(kNT),
+                           0, s, a + b0 * n, b + b0 * n, n, (int)h, p.M, f);
+      }
+    }
+    double* t = a;
+    a = b;
+    b = t;
+  }
+  if (a != out)
+    JW_HIP_TRY(hipMemcpyAsync(out, a, sizeof(double) * n * batch, hipMemcpyDeviceToDevice, s));
+  JW_HIP_TRY(hipGetLastError());
+  JW_HIP_TRY(hipFreeAsync(tmp, s));
+  return JW_OK;
+}
+
+}  // namespace
+
+int wpt_forward_device(const FwtPlan& p, const double* x, double* y, long n, int level, int batch,
+                       hipStream_t s) {
+  return p.arith == JW_ARITH_FMA ? wpt_t<true>(p, false, x, y, n, level, batch, s)
+                                 : wpt_t<false>(p, false, x, y, n, level, batch, s);
+}
+
+int wpt_reverse_device(const FwtPlan& p, const double* y, double* x, long n, int level, int batch,
+                       hipStream_t s) {
+  return p.arith == JW_ARITH_FMA ? wpt_t<true>(p, true, y, x, n, level, batch, s)
+                                 : wpt_t<false>(p, true, y, x, n, level, batch, s);
 }
 
 // 2-D (BasicTransform.java:361-399): every row with lvlN, then every column with lvlM.

@@ -63,6 +63,10 @@ int modwt_inverse_fft_device(const ModwtPlan& p, const double* coeffs, double* x
 int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
                    const double* scales_host, int ns, double fs, int padding, double* out,
                    int batch, hipStream_t s);
+int wpt_forward_device(const FwtPlan& p, const double* x, double* y, long n, int level, int batch,
+                       hipStream_t s);
+int wpt_reverse_device(const FwtPlan& p, const double* y, double* x, long n, int level, int batch,
+                       hipStream_t s);
 int fwt_forward_device(const FwtPlan& p, const double* x, double* y, long n, int level, int batch,
                        hipStream_t s);
 int fwt_reverse_device(const FwtPlan& p, const double* y, double* x, long n, int level, int batch,

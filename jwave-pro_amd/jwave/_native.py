@@ -45,7 +45,7 @@ EXPORTS = (
     "jw_modwt_forward", "jw_modwt_inverse",
     "jw_fwt_plan_create", "jw_fwt_plan_destroy", "jw_fwt_forward", "jw_fwt_reverse",
     "jw_fwt2d_forward", "jw_fwt2d_reverse",
-    "jw_synth_uniform", "jw_cwt_fft",
+    "jw_synth_uniform", "jw_cwt_fft", "jw_wpt_forward", "jw_wpt_reverse",
 )
 
 _lib = None
@@ -86,6 +86,8 @@ def lib():
     L.jw_fwt_plan_destroy.restype = None
     L.jw_fwt_forward.argtypes = [c_dp, c_dp, c_dp, l, i, i, i, c_dp]
     L.jw_fwt_reverse.argtypes = [c_dp, c_dp, c_dp, l, i, i, i, c_dp]
+    L.jw_wpt_forward.argtypes = [c_dp, c_dp, c_dp, l, i, i, i, c_dp]
+    L.jw_wpt_reverse.argtypes = [c_dp, c_dp, c_dp, l, i, i, i, c_dp]
     L.jw_fwt2d_forward.argtypes = [c_dp, c_dp, c_dp, i, i, i, i, i, i, c_dp]
     L.jw_fwt2d_reverse.argtypes = [c_dp, c_dp, c_dp, i, i, i, i, i, i, c_dp]
     L.jw_synth_uniform.argtypes = [c_dp, l, i, l, c_dp]

@@ -163,3 +163,41 @@ class FastWaveletTransform(WaveletTransform):
         if level < 0 or level >= len(matDeComp):
             raise JWaveFailure("WaveletTransform#recompose - given level is out of range")
         return self.reverse(np.asarray(matDeComp[level], dtype=np.float64), level)
+
+
+class WaveletPacketTransform(FastWaveletTransform):
+    """jwave.transforms.WaveletPacketTransform (WaveletPacketTransform.java:60-191): every level
+    transforms all packets.  1-D through jw_wpt_forward / jw_wpt_reverse; the 2-D methods
+    (BasicTransform.java:361-474) run the 1-D packet transform over rows, then columns."""
+
+    def __init__(self, wavelet, arith="strict"):
+        super().__init__(wavelet, arith)
+        self._name = "Wavelet Packet Transform"
+
+    def _run1d(self, a, level, batch, reverse):
+        L = _native.lib()
+        n = a.shape[-1]
+        B = a.shape[0] if batch else 1
+        out = a.empty(a.shape)
+        fn = L.jw_wpt_reverse if reverse else L.jw_wpt_forward
+        _native.check(fn(self._plan, a.ptr, out.ptr, n, int(level), B, a.where, a.stream))
+        return out.result()
+
+    def _rows(self, m, level, reverse):
+        return self._run1d(as_input(m), level, batch=True, reverse=reverse)
+
+    @staticmethod
+    def _t(m):
+        return m.t().contiguous() if hasattr(m, "is_cuda") else np.ascontiguousarray(m.T)
+
+    def _forward2d(self, mat, lvlM, lvlN, batch=False):
+        if batch:
+            return [self._forward2d(m, lvlM, lvlN) for m in mat]
+        y = self._rows(mat, lvlN, False)
+        return self._t(self._rows(self._t(y), lvlM, False))
+
+    def _reverse2d(self, mat, lvlM, lvlN, batch=False):
+        if batch:
+            return [self._reverse2d(m, lvlM, lvlN) for m in mat]
+        x = self._t(self._rows(self._t(mat), lvlM, True))
+        return self._rows(x, lvlN, True)

@@ -430,6 +430,43 @@ void jwo_fwt_reverse(const double* y, long n, int level, const double* sR, const
   free(tmp);
 }
 
+/* WaveletPacketTransform.forward :60-117 / reverse :119-191: every packet of the level */
+void jwo_wpt_forward(const double* x, long n, int level, const double* sD, const double* wD,
+                     int M, int tw, double* y) {
+  double* tmp = (double*)malloc(sizeof(double) * (n > 0 ? n : 1));
+  memcpy(y, x, sizeof(double) * n);
+  long k = n, h = n;
+  int l = 0;
+  while (h >= tw && l < level) {
+    long g = k / h;
+    for (long p = 0; p < g; p++) {
+      jwo_wavelet_forward(y + p * h, (int)h, sD, wD, M, tmp);
+      memcpy(y + p * h, tmp, sizeof(double) * h);
+    }
+    h = h >> 1;
+    l++;
+  }
+  free(tmp);
+}
+
+void jwo_wpt_reverse(const double* y, long n, int level, const double* sR, const double* wR,
+                     int M, int tw, int kind, double* x) {
+  double* tmp = (double*)malloc(sizeof(double) * (n > 0 ? n : 1));
+  memcpy(x, y, sizeof(double) * n);
+  long k = n, h = tw;
+  int steps = java_get_exponent((double)n);
+  for (int l = level; l < steps; l++) h = h << 1;
+  while (h <= n && h >= tw) {
+    long g = k / h;
+    for (long p = 0; p < g; p++) {
+      jwo_wavelet_reverse(x + p * h, (int)h, sR, wR, M, kind, tmp);
+      memcpy(x + p * h, tmp, sizeof(double) * h);
+    }
+    h = h << 1;
+  }
+  free(tmp);
+}
+
 void jwo_fwt2d_forward(const double* x, int rows, int cols, int lvlM, int lvlN, const double* sD,
                        const double* wD, int M, int tw, double* y) {
   int mx = rows > cols ? rows : cols;

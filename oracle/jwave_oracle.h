@@ -78,6 +78,10 @@ void jwo_fwt_forward(const double* x, long n, int level, const double* sD, const
 void jwo_fwt_reverse(const double* y, long n, int level, const double* sR, const double* wR,
                      int M, int tw, int kind, double* x);
 /* BasicTransform.forward/reverse(double[][], lvlM, lvlN) (BasicTransform.java:361-474). */
+void jwo_wpt_forward(const double* x, long n, int level, const double* sD, const double* wD,
+                     int M, int tw, double* y);
+void jwo_wpt_reverse(const double* y, long n, int level, const double* sR, const double* wR,
+                     int M, int tw, int kind, double* x);
 void jwo_fwt2d_forward(const double* x, int rows, int cols, int lvlM, int lvlN, const double* sD,
                        const double* wD, int M, int tw, double* y);
 void jwo_fwt2d_reverse(const double* y, int rows, int cols, int lvlM, int lvlN, const double* sR,

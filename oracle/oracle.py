@@ -119,6 +119,24 @@ def fwt_reverse(y, level, wavelet):
     return x
 
 
+def wpt_forward(x, level, wavelet):
+    x = _f64(x)
+    y = np.empty_like(x)
+    sD, wD = _f64(wavelet.getScalingDeComposition()), _f64(wavelet.getWaveletDeComposition())
+    lib().jwo_wpt_forward(_p(x), ctypes.c_long(x.shape[0]), level, _p(sD), _p(wD), sD.shape[0],
+                          wavelet.getTransformWavelength(), _p(y))
+    return y
+
+
+def wpt_reverse(y, level, wavelet):
+    y = _f64(y)
+    x = np.empty_like(y)
+    sR, wR = _f64(wavelet.getScalingReConstruction()), _f64(wavelet.getWaveletReConstruction())
+    lib().jwo_wpt_reverse(_p(y), ctypes.c_long(y.shape[0]), level, _p(sR), _p(wR), sR.shape[0],
+                          wavelet.getTransformWavelength(), getattr(wavelet, "kind", 0), _p(x))
+    return x
+
+
 def fwt2d_forward(x, lvlM, lvlN, wavelet):
     x = _f64(x)
     y = np.empty_like(x)

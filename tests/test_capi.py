@@ -203,3 +203,15 @@ def test_cwt_result_accessors():
     assert r.getNumberOfScales() == 2 and r.getNumberOfTimePoints() == 4
     with pytest.raises(IndexError):
         r.getCoefficientsAtScale(2)
+
+
+def test_wpt_validation_messages():
+    # WaveletPacketTransform.java:63-72 / :122-131 (checked JWaveFailure, exact text)
+    from jwave import WaveletPacketTransform
+    t = WaveletPacketTransform(W.Daubechies4())
+    with pytest.raises(JWaveFailure, match="given array length is not 2"):
+        t.forward(np.ones(6), 1)
+    with pytest.raises(JWaveFailure, match="WaveletPacketTransform#forward - given level is out"):
+        t.forward(np.ones(8), 4)
+    with pytest.raises(JWaveFailure, match="WaveletPacketTransform#reverse - given level is out"):
+        t.reverse(np.ones(8), -1)

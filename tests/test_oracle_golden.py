@@ -234,3 +234,39 @@ def test_modwt_nonzero_tap_variant_is_bit_identical(wname, n, J):
     c = orc.modwt_forward(x, J, g, h, "direct")
     assert bits_equal(c, orc.modwt_forward(x, J, g, h, "direct_nz"))
     assert bits_equal(orc.modwt_inverse(c, g, h, "direct"), orc.modwt_inverse(c, g, h, "direct_nz"))
+
+
+# ---------------------------------------------------------------- WPT
+@pytest.mark.parametrize("wname", CREATE2ARR)
+def test_wpt_stepping_constant(wname):
+    # SteppingTest.java:180-215: WPT of {1,1,1,1} at levels 0..2, delta 1e-8, and reverse
+    wv = W.by_name(wname)
+    s2 = math.sqrt(2.)
+    x = np.ones(4)
+    for lvl, exp in enumerate([[1, 1, 1, 1], [s2, s2, 0, 0], [2, 0, 0, 0]]):
+        y = orc.wpt_forward(x, lvl, wv)
+        assert np.max(np.abs(y - exp)) < 1e-8
+        assert np.max(np.abs(orc.wpt_reverse(y, lvl, wv) - x)) < 1e-8
+
+
+def test_wpt_transforms_every_packet():
+    # WaveletPacketTransform.java:86-108: at level 2 both halves of level 1 are transformed --
+    # the second half of the packet transform is the FWT of the level-1 detail half
+    wv = W.Daubechies4()
+    x = orc.fill_uniform(64, 3)
+    l1 = orc.fwt_forward(x, 1, wv)
+    l2 = orc.wpt_forward(x, 2, wv)
+    assert bits_equal(l2[:32], orc.fwt_forward(l1[:32], 1, wv))
+    assert bits_equal(l2[32:], orc.fwt_forward(l1[32:], 1, wv))
+
+
+@pytest.mark.parametrize("wname", ["Haar1", "Daubechies4", "Symlet8", "Haar1Orthogonal",
+                                   "Legendre2"])
+def test_wpt_rounding(wname):
+    # RoundingTest.java:160-204: 256 forward+reverse WPT of ones(1024) within 1e-8
+    wv = W.by_name(wname) if wname != "Haar1Orthogonal" else W.Haar1Orthogonal()
+    x = np.ones(1024)
+    y = x.copy()
+    for _ in range(256):
+        y = orc.wpt_reverse(orc.wpt_forward(y, 10, wv), 10, wv)
+    assert np.max(np.abs(y - x)) < 1e-8
