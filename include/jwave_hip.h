@@ -117,6 +117,10 @@ int jw_fwt2d_reverse(const jw_fwt_plan* plan, const double* y, double* x, int ro
  * ====================================================================== */
 #define JW_CWT_MORLET 0 /* MorletWavelet(fb, fc): params = {fb, fc} (MorletWavelet.java:66-124) */
 #define JW_CWT_MEXHAT 1 /* MexicanHatWavelet(sigma): params = {sigma} (MexicanHatWavelet.java) */
+#define JW_CWT_PAUL 2   /* PaulWavelet(m): params = {m}, integer 1..20 (PaulWavelet.java:76-99) */
+#define JW_CWT_DOG 3    /* DOGWavelet(n, sigma): params = {n, sigma}, n integer 1..10
+                           (DOGWavelet.java:129-157) */
+#define JW_CWT_MEYER 4  /* MeyerWavelet(): no parameters (MeyerWavelet.java:164-169) */
 /* ContinuousWaveletTransform.PaddingType (ContinuousWaveletTransform.java:74-79) */
 #define JW_PAD_ZERO 0
 #define JW_PAD_SYMMETRIC 1
@@ -127,8 +131,10 @@ int jw_fwt2d_reverse(const jw_fwt_plan* plan, const double* y, double* x, int ro
  * for batch signals x (batch x n); out_reim: batch x ns x n complex, interleaved (re, im).
  * scales: host array of ns positive scales (read at call time).  The padded length is
  * nextPowerOfTwo(n) <= 2^24.  Parameter checks follow the Java constructors:
- * fb, fc, sigma > 0 ("Bandwidth parameter must be positive", ...), scales > 0
- * ("Scale must be positive"). */
+ * fb, fc, sigma > 0 ("Bandwidth parameter must be positive", ...), Paul m and DOG n in range
+ * ("Order parameter m must be a positive integer", ...), scales > 0 ("Scale must be positive";
+ * not for Paul, whose fourierTransform(omega, scale, b) override :152-164 does not check).
+ * psi_hat is complex for DOG with odd n and for Meyer; the product is X * conj(psi_hat). */
 int jw_cwt_fft(int wavelet, const double* params, const double* x, long n, const double* scales,
                int ns, double sampling_rate, int padding, double* out_reim, int batch, int where,
                void* stream);

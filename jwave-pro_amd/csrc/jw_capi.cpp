@@ -380,21 +380,40 @@ int jw_cwt_fft(int wavelet, const double* params, const double* x, long n, const
                int ns, double sampling_rate, int padding, double* out_reim, int batch, int where,
                void* stream) {
   clear_error();
-  if (wavelet != JW_CWT_MORLET && wavelet != JW_CWT_MEXHAT)
+  if (wavelet < JW_CWT_MORLET || wavelet > JW_CWT_MEYER)
     return fail(JW_ERR_ILLEGAL_ARGUMENT, "unknown continuous wavelet kind %d", wavelet);
-  if (!params) return fail(JW_ERR_ILLEGAL_ARGUMENT, "wavelet parameters are null");
+  if (!params && wavelet != JW_CWT_MEYER)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "wavelet parameters are null");
+  // an integer order carried in a double (the Java constructors take int)
+  auto order = [](double v, int hi, const char* lo_msg, const char* hi_msg) -> int {
+    if (!(v >= 1) || v != std::floor(v)) return fail(JW_ERR_ILLEGAL_ARGUMENT, "%s", lo_msg);
+    if (v > hi) return fail(JW_ERR_ILLEGAL_ARGUMENT, "%s", hi_msg);
+    return JW_OK;
+  };
   if (wavelet == JW_CWT_MORLET) {  // MorletWavelet.java:69-74
     if (!(params[0] > 0)) return fail(JW_ERR_ILLEGAL_ARGUMENT, "Bandwidth parameter must be positive");
     if (!(params[1] > 0)) return fail(JW_ERR_ILLEGAL_ARGUMENT, "Center frequency must be positive");
-  } else if (!(params[0] > 0)) {  // MexicanHatWavelet.java:67-69
-    return fail(JW_ERR_ILLEGAL_ARGUMENT, "Width parameter sigma must be positive");
+  } else if (wavelet == JW_CWT_MEXHAT) {  // MexicanHatWavelet.java:67-69
+    if (!(params[0] > 0))
+      return fail(JW_ERR_ILLEGAL_ARGUMENT, "Width parameter sigma must be positive");
+  } else if (wavelet == JW_CWT_PAUL) {  // PaulWavelet.java:79-84
+    const int st = order(params[0], 20, "Order parameter m must be a positive integer",
+                         "Order parameter m > 20 may cause numerical issues");
+    if (st != JW_OK) return st;
+  } else if (wavelet == JW_CWT_DOG) {  // DOGWavelet.java:132-140
+    const int st = order(params[0], 10, "Derivative order n must be a positive integer",
+                         "Derivative order n > 10 may cause numerical issues");
+    if (st != JW_OK) return st;
+    if (!(params[1] > 0))
+      return fail(JW_ERR_ILLEGAL_ARGUMENT, "Width parameter sigma must be positive");
   }
   if (n < 0 || ns < 0 || batch < 0)
     return fail(JW_ERR_ILLEGAL_ARGUMENT, "negative size (n=%ld, ns=%d, batch=%d)", n, ns, batch);
   if (padding < JW_PAD_ZERO || padding > JW_PAD_CONSTANT)
     return fail(JW_ERR_ILLEGAL_ARGUMENT, "unknown padding type %d", padding);
   if (n > 0 && ns > 0 && !scales) return fail(JW_ERR_ILLEGAL_ARGUMENT, "scales are null");
-  for (int i = 0; i < ns && n > 0; ++i)  // ContinuousWavelet.fourierTransform :123-125
+  // ContinuousWavelet.fourierTransform :123-125 (PaulWavelet's override :152-164 has no check)
+  for (int i = 0; i < ns && n > 0 && wavelet != JW_CWT_PAUL; ++i)
     if (!(scales[i] > 0)) return fail(JW_ERR_ILLEGAL_ARGUMENT, "Scale must be positive");
   int st = check_where(where);
   if (st != JW_OK) return st;

@@ -6,14 +6,17 @@
 // scale a: coeff[a][t] = IFFT(X * conj(psi_hat(omega, a, 0)))[t] for t < n, with
 // omega[i] = 2 pi i fs / Np - [i > Np/2] 2 pi fs (createFrequencyAxis :450-459) and
 // psi_hat(omega, a, 0) = F(a omega) sqrt(a) (ContinuousWavelet.fourierTransform :122-141).
-// psi_hat is real for Morlet (MorletWavelet.java:112-124) and Mexican Hat
-// (MexicanHatWavelet.java:107-119), evaluated per bin inside the first IFFT pass (never stored).
+// psi_hat is evaluated per bin inside the first IFFT pass (never stored): real for Morlet
+// (MorletWavelet.java:112-124), Mexican Hat (MexicanHatWavelet.java:107-119) and Paul
+// (PaulWavelet.java:152-164), complex for DOG (DOGWavelet.java:187-220, odd n) and Meyer
+// (MeyerWavelet.java:223-253).
 //
 // HBM: the spectra X (B x Np complex) stay resident; each (signal, scale) IFFT is two passes
 // through a group workspace A (G pairs x Np complex) that the Infinity Cache mostly absorbs;
 // the coefficients (B x ns x n complex) are written once -- that write is the roofline.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "jw_fft_passes.hpp"
 
@@ -33,26 +36,70 @@ using fft::tpos;
 constexpr double kPi = 3.14159265358979323846;  // Math.PI
 
 struct WaveletFT {
-  int kind;        // JW_CWT_MORLET / JW_CWT_MEXHAT
-  double p0, p1;   // Morlet (fb, fc); Mexican Hat (sigma, unused)
-  double norm;     // Morlet sqrt(2 pi fb); Mexican Hat ftNorm = nc sigma sqrt(2 pi)
+  int kind;        // JW_CWT_*
+  int ord;         // Paul m, DOG n
+  double p0, p1;   // Morlet (fb, fc); Mexican Hat and DOG (sigma, unused)
+  double norm;     // Morlet sqrt(2 pi fb); Mexican Hat ftNorm = nc sigma sqrt(2 pi);
+                   // Paul and Meyer sqrt(2 pi); DOG sqrt(2 pi) sigma^(n+1)
+  double norm2;    // DOG _normConstant (computeNormalizationConstant :357-366)
 };
 
-// F(a omega) * sqrt(a), in the reference's operation order.
-__device__ __forceinline__ double psi_hat(const WaveletFT& w, double omega, double scale,
-                                          double sqrt_scale) {
+// Meyer transition polynomial nu(x) = x^4 (35 - 84x + 70x^2 - 20x^3) (MeyerWavelet.java:279-295)
+__device__ __forceinline__ double meyer_nu(double x) {
+  if (x <= 0) return 0.0;
+  if (x >= 1) return 1.0;
+  const double x2 = x * x, x3 = x2 * x, x4 = x3 * x;
+  return x4 * (35.0 + -84.0 * x + 70.0 * x2 + -20.0 * x3);
+}
+
+// psi_hat(omega, a, 0) = sqrt(a) F(a omega) as (re, im), in the reference's operation order.
+// The exp arguments below -746 give +0 in Java as here; the test only skips the exp call.
+template <int K>
+__device__ __forceinline__ cplx psi_hat(const WaveletFT& w, double omega, double scale,
+                                        double sqrt_scale) {
   const double om = scale * omega;  // fourierTransform(scale * omega)
-  double v;
-  if (w.kind == JW_CWT_MORLET) {
+  double re = 0.0, im = 0.0;
+  if constexpr (K == JW_CWT_MORLET) {  // MorletWavelet.java:114-124
     const double f = om / (2.0 * kPi);
     const double e = -2.0 * kPi * kPi * w.p0 * (f - w.p1) * (f - w.p1);
-    v = e < -746.0 ? 0.0 : w.norm * exp(e);  // exp underflows to +0 below -745.2 anyway
-  } else {
+    re = e < -746.0 ? 0.0 : w.norm * exp(e);
+  } else if constexpr (K == JW_CWT_MEXHAT) {  // MexicanHatWavelet.java:107-119
     const double om2 = om * om;
     const double e = -0.5 * w.p0 * w.p0 * om2;
-    v = e < -746.0 ? 0.0 : w.norm * om2 * exp(e);
+    re = e < -746.0 ? 0.0 : w.norm * om2 * exp(e);
+  } else if constexpr (K == JW_CWT_PAUL) {
+    // PaulWavelet.fourierTransform(omega, scale, b) override :152-164: no sqrt(a) afterwards
+    if (omega <= 0) return make_double2(0.0, 0.0);
+    if (-om < -746.0) return make_double2(0.0, 0.0);
+    return make_double2(sqrt_scale * w.norm * pow(om, (double)w.ord) * exp(-om), 0.0);
+  } else if constexpr (K == JW_CWT_DOG) {  // DOGWavelet.java:187-220
+    const double e = -0.5 * w.p0 * w.p0 * om * om;
+    double mag = e < -746.0 ? 0.0 : w.norm * pow(fabs(om), (double)w.ord) * exp(e);
+    mag *= w.norm2;
+    const double sg = om > 0 ? 1.0 : (om < 0 ? -1.0 : om);  // Math.signum
+    switch (w.ord & 3) {
+      case 0: re = mag; break;
+      case 1: im = mag * sg; break;
+      case 2: re = -mag; break;
+      default: im = -mag * sg; break;
+    }
+  } else {  // Meyer, MeyerWavelet.java:223-253
+    constexpr double lo = 2.0 * kPi / 3.0, mid = 4.0 * kPi / 3.0, hi = 8.0 * kPi / 3.0;
+    const double a = fabs(om);
+    if (a < lo || a > hi) return make_double2(0.0, 0.0);
+    double v;
+    if (a <= mid) {
+      v = sin(kPi / 2.0 * meyer_nu(3.0 * a / (2.0 * kPi) - 1.0));
+    } else {
+      v = cos(kPi / 2.0 * meyer_nu(3.0 * a / (4.0 * kPi) - 1.0));
+    }
+    v *= w.norm;
+    double sn, cs;
+    sincos(om / 2.0, &sn, &cs);
+    re = v * cs;
+    im = v * sn;
   }
-  return v * sqrt_scale;  // ft.mul(Math.sqrt(scale))
+  return make_double2(re * sqrt_scale, im * sqrt_scale);  // ft.mul(Math.sqrt(scale))
 }
 
 
@@ -82,7 +129,8 @@ struct PadIn {  // padded real signal, element k (padSignal :269-306)
     return make_double2(v, 0.0);
   }
 };
-struct ScaleIn {  // X[sig][k] * psi_hat(omega_k, a_s), k = N2 k1 + col; item = pair in group
+template <int K>
+struct ScaleIn {  // X[sig][k] * conj(psi_hat(omega_k, a_s)), k = N2 k1 + col; item = pair in group
   static constexpr bool kStrided = false;  // column-major spectra: contiguous columns
   const cplx* X;
   const double* scales;
@@ -97,10 +145,15 @@ struct ScaleIn {  // X[sig][k] * psi_hat(omega_k, a_s), k = N2 k1 + col; item = 
     double om = 2.0 * kPi * (double)k * fs / (double)N;  // createFrequencyAxis :453-456
     if (k > N / 2) om -= 2.0 * kPi * fs;
     const double a = scales[s];
-    const double wv = psi_hat(w, om, a, sqrt(a));
-    if (wv == 0.0) return make_double2(0.0, 0.0);  // exp underflowed: skip the X read
+    const cplx wv = psi_hat<K>(w, om, a, sqrt(a));
+    if (wv.x == 0.0 && wv.y == 0.0) return make_double2(0.0, 0.0);  // skip the X read
     const cplx xv = X[sig * N + col * N1 + k1];
-    return make_double2(xv.x * wv, xv.y * wv);  // signalFFT[i].mul(conj(waveletFFT[i]))
+    if constexpr (K == JW_CWT_DOG || K == JW_CWT_MEYER) {
+      const double cr = wv.x, ci = -wv.y;  // waveletFFT[i].conjugate(); signalFFT[i].mul(...)
+      return make_double2(xv.x * cr - xv.y * ci, xv.x * ci + xv.y * cr);
+    } else {  // real psi_hat: the imaginary products are exact zeros
+      return make_double2(xv.x * wv.x, xv.y * wv.x);
+    }
   }
 };
 struct CoefOut {  // out[pair][t] = v / N for t = line + N1 * idx < n  (reverse :207-211)
@@ -137,15 +190,29 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   Tables T;
   int st = fft::tables(N, &T);
   if (st != JW_OK) return st;
-  WaveletFT w;
+  WaveletFT w{};
   w.kind = wavelet;
-  w.p0 = params[0];
-  w.p1 = wavelet == JW_CWT_MORLET ? params[1] : 0.0;
   if (wavelet == JW_CWT_MORLET) {
+    w.p0 = params[0];
+    w.p1 = params[1];
     w.norm = std::sqrt(2.0 * kPi * w.p0);  // MorletWavelet.java:117
-  } else {
+  } else if (wavelet == JW_CWT_MEXHAT) {
+    w.p0 = params[0];
     const double nc = 2.0 / (std::sqrt(3.0 * w.p0) * std::pow(kPi, 0.25));  // :72
     w.norm = nc * w.p0 * std::sqrt(2.0 * kPi);                              // :111
+  } else if (wavelet == JW_CWT_PAUL) {
+    w.ord = (int)params[0];
+    w.norm = std::sqrt(2.0 * kPi);  // PaulWavelet.java:159
+  } else if (wavelet == JW_CWT_DOG) {
+    w.ord = (int)params[0];
+    w.p0 = params[1];
+    w.norm = std::sqrt(2.0 * kPi) * std::pow(w.p0, w.ord + 1);  // DOGWavelet.java:189-190
+    double df = 1.0;  // doubleFactorial(2n - 1) :376-382
+    for (int i = 2 * w.ord - 1; i > 0; i -= 2) df *= i;
+    w.norm2 = std::sqrt(df / (std::pow(2, w.ord) * std::sqrt(kPi) *
+                              std::pow(w.p0, 2 * w.ord + 1)));  // :357-366
+  } else {
+    w.norm = std::sqrt(2.0 * kPi);  // MeyerWavelet.java:244
   }
   const char* gnt = std::getenv("JW_CWT_NT");  // A/B runs: bit 1 = NT stores of A, 2 = of coeffs
   const int ntm = gnt ? std::atoi(gnt) : 2;  // measured best: NT coefficient stores only
@@ -173,10 +240,19 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   const long pairs = (long)batch * ns;
   for (long p0 = 0; p0 < pairs && st == JW_OK; p0 += gpair) {
     const long np_ = std::min<long>(gpair, pairs - p0);
-    ScaleIn in{X, dsc, w, N, N1, N <= 4096 ? 1 : N / N1, p0, ns, fs};
     CoefOut o{out, n, N <= 4096 ? 1 : N1, p0, 1.0 / (double)N, (ntm & 2) != 0};
     CoefOut o1{out, n, 1, p0, 1.0 / (double)N, (ntm & 2) != 0};
-    st = run_fft<1>(N, np_, in, o1, o, A, s, T, (ntm & 1) != 0);
+    auto go = [&](auto kind) {
+      ScaleIn<decltype(kind)::value> in{X, dsc, w, N, N1, N <= 4096 ? 1 : N / N1, p0, ns, fs};
+      return run_fft<1>(N, np_, in, o1, o, A, s, T, (ntm & 1) != 0);
+    };
+    switch (wavelet) {
+      case JW_CWT_MORLET: st = go(std::integral_constant<int, JW_CWT_MORLET>{}); break;
+      case JW_CWT_MEXHAT: st = go(std::integral_constant<int, JW_CWT_MEXHAT>{}); break;
+      case JW_CWT_PAUL: st = go(std::integral_constant<int, JW_CWT_PAUL>{}); break;
+      case JW_CWT_DOG: st = go(std::integral_constant<int, JW_CWT_DOG>{}); break;
+      default: st = go(std::integral_constant<int, JW_CWT_MEYER>{}); break;
+    }
   }
   (void)hipFreeAsync(dsc, s);
   (void)hipFreeAsync(A, s);

@@ -171,7 +171,6 @@ __global__ __launch_bounds__(kNT) void fwt_rev_lds(const double* __restrict__ y,
 typedef double d2 __attribute__((ext_vector_type(2)));
 
 constexpr int kNT2 = 256;               // fast LDS cascades: 4 waves per row
-constexpr int kPer2 = kLdsN / kNT2;
 
 // Outputs (2u, 2u+1) that see wrapped taps, in Java's scatter order (i ascending, then j),
 // with compile-time M: fully unrolled, predicated (select, not "+ 0.0") so the sums are

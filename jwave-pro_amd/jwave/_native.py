@@ -23,6 +23,9 @@ JW_DEVICE = 1
 
 JW_CWT_MORLET = 0
 JW_CWT_MEXHAT = 1
+JW_CWT_PAUL = 2
+JW_CWT_DOG = 3
+JW_CWT_MEYER = 4
 JW_PAD_ZERO = 0
 JW_PAD_SYMMETRIC = 1
 JW_PAD_PERIODIC = 2

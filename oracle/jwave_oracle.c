@@ -502,25 +502,76 @@ void jwo_fwt2d_reverse(const double* y, int rows, int cols, int lvlM, int lvlN, 
 /* ------------------------------------------------------------------------ */
 /* CWT FFT path: ContinuousWaveletTransform.transformFFT :183-229, padSignal :269-306, */
 /* createFrequencyAxis :450-459, ContinuousWavelet.fourierTransform :122-141,          */
-/* MorletWavelet.fourierTransform :114-124, MexicanHatWavelet :65-119.                */
+/* MorletWavelet.fourierTransform :114-124, MexicanHatWavelet :65-119, Paul / DOG / Meyer. */
 /* ------------------------------------------------------------------------ */
-double jwo_cwt_wavelet_ft(int wavelet, const double* params, double omega, double scale) {
+static double meyer_nu(double x) { /* MeyerWavelet.transitionFunction :279-295 */
+  if (x <= 0) return 0.0;
+  if (x >= 1) return 1.0;
+  double x2 = x * x, x3 = x2 * x, x4 = x3 * x;
+  return x4 * (35.0 + -84.0 * x + 70.0 * x2 + -20.0 * x3);
+}
+
+/* F[psi_{a,0}](omega) as (re, im).  Kinds: 0 Morlet {fb, fc}, 1 Mexican Hat {sigma},
+ * 2 Paul {m} (PaulWavelet.java:76-99, override :152-164), 3 DOG {n, sigma}
+ * (DOGWavelet.java:129-220, 357-382), 4 Meyer {} (MeyerWavelet.java:223-295). */
+void jwo_cwt_wavelet_ft_c(int wavelet, const double* params, double omega, double scale,
+                          double* re_out, double* im_out) {
   double w = scale * omega; /* fourierTransform(scale * omega) */
-  double value;
+  double re = 0.0, im = 0.0;
   if (wavelet == 0) {
     double fb = params[0], fc = params[1];
     double f = w / (2.0 * JAVA_PI);
     double norm = sqrt(2.0 * JAVA_PI * fb);
     double exponent = -2.0 * JAVA_PI * JAVA_PI * fb * (f - fc) * (f - fc);
-    value = norm * exp(exponent);
-  } else {
+    re = norm * exp(exponent);
+  } else if (wavelet == 1) {
     double sigma = params[0];
     double nc = 2.0 / (sqrt(3.0 * sigma) * pow(JAVA_PI, 0.25));
     double ftNorm = nc * sigma * sqrt(2.0 * JAVA_PI);
     double omega2 = w * w;
-    value = ftNorm * omega2 * exp(-0.5 * sigma * sigma * omega2);
+    re = ftNorm * omega2 * exp(-0.5 * sigma * sigma * omega2);
+  } else if (wavelet == 2) { /* the override returns without a further sqrt(scale) */
+    int m = (int)params[0];
+    *re_out = omega <= 0 ? 0.0 : sqrt(scale) * sqrt(2.0 * JAVA_PI) * pow(w, m) * exp(-w);
+    *im_out = 0.0;
+    return;
+  } else if (wavelet == 3) {
+    int n = (int)params[0];
+    double sigma = params[1];
+    double df = 1.0;
+    for (int i = 2 * n - 1; i > 0; i -= 2) df *= i;
+    double nc = sqrt(df / (pow(2, n) * sqrt(JAVA_PI) * pow(sigma, 2 * n + 1)));
+    double mag = sqrt(2.0 * JAVA_PI) * pow(sigma, n + 1) * pow(fabs(w), n) *
+                 exp(-0.5 * sigma * sigma * w * w);
+    mag *= nc;
+    double sg = w > 0 ? 1.0 : (w < 0 ? -1.0 : w); /* Math.signum */
+    switch (n % 4) {
+      case 0: re = mag; break;
+      case 1: im = mag * sg; break;
+      case 2: re = -mag; break;
+      default: im = -mag * sg; break;
+    }
+  } else {
+    double a = fabs(w), v = 0.0;
+    if (a >= 2.0 * JAVA_PI / 3.0 && a <= 8.0 * JAVA_PI / 3.0) {
+      if (a <= 4.0 * JAVA_PI / 3.0) {
+        v = sin(JAVA_PI / 2.0 * meyer_nu(3.0 * a / (2.0 * JAVA_PI) - 1.0));
+      } else {
+        v = cos(JAVA_PI / 2.0 * meyer_nu(3.0 * a / (4.0 * JAVA_PI) - 1.0));
+      }
+      v *= sqrt(2.0 * JAVA_PI);
+      re = v * cos(w / 2.0);
+      im = v * sin(w / 2.0);
+    }
   }
-  return value * sqrt(scale); /* ft.mul(Math.sqrt(scale)) (real part) */
+  *re_out = re * sqrt(scale); /* ft.mul(Math.sqrt(scale)) */
+  *im_out = im * sqrt(scale);
+}
+
+double jwo_cwt_wavelet_ft(int wavelet, const double* params, double omega, double scale) {
+  double re, im;
+  jwo_cwt_wavelet_ft_c(wavelet, params, omega, scale, &re, &im);
+  return re;
 }
 
 void jwo_cwt_fft(int wavelet, const double* params, const double* x, long n,
@@ -551,9 +602,9 @@ void jwo_cwt_fft(int wavelet, const double* params, const double* x, long n,
   for (int s = 0; s < ns; s++) {
     double scale = scales[s];
     for (long i = 0; i < np; i++) {
-      double wr = jwo_cwt_wavelet_ft(wavelet, params, omega[i], scale);
-      double wi = 0.0 * sqrt(scale); /* imaginary part of ft.mul(sqrt(a)) */
-      wi = -wi;                      /* conjugate() */
+      double wr, wi;
+      jwo_cwt_wavelet_ft_c(wavelet, params, omega[i], scale, &wr, &wi);
+      wi = -wi; /* conjugate() */
       double sr = X[2 * i], si = X[2 * i + 1];
       P[2 * i] = sr * wr - si * wi;
       P[2 * i + 1] = sr * wi + si * wr;

@@ -88,12 +88,15 @@ void jwo_fwt2d_reverse(const double* y, int rows, int cols, int lvlM, int lvlN, 
                        const double* wR, int M, int tw, int kind, double* x);
 
 /* ---- CWT FFT path (transforms/ContinuousWaveletTransform.java:183-229) ---- */
-/* wavelet: 0 = Morlet(params[0]=fb, params[1]=fc), 1 = MexicanHat(params[0]=sigma)
+/* wavelet: 0 = Morlet(params[0]=fb, params[1]=fc), 1 = MexicanHat(params[0]=sigma),
+ * 2 = Paul(params[0]=m), 3 = DOG(params[0]=n, params[1]=sigma), 4 = Meyer()
  * padding: 0 ZERO, 1 SYMMETRIC, 2 PERIODIC, 3 CONSTANT.  out: ns x n x 2 (re,im). */
 void jwo_cwt_fft(int wavelet, const double* params, const double* x, long n,
                  const double* scales, int ns, double fs, int padding, double* out_reim);
 /* ContinuousWavelet.fourierTransform(omega, scale, 0) (ContinuousWavelet.java:122-141). */
 double jwo_cwt_wavelet_ft(int wavelet, const double* params, double omega, double scale);
+void jwo_cwt_wavelet_ft_c(int wavelet, const double* params, double omega, double scale,
+                          double* re, double* im);
 
 /* ---- batched wrappers for the CPU baseline (ForkJoin-equivalent, OpenMP over signals) ---- */
 void jwo_modwt_fwdinv_batch(const double* x, long N, int J, const double* g, const double* h,

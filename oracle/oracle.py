@@ -156,16 +156,30 @@ def fwt2d_reverse(y, lvlM, lvlN, wavelet):
     return x
 
 
+CWT_KINDS = {"morlet": 0, "mexhat": 1, "paul": 2, "dog": 3, "meyer": 4}
+
+
+def cwt_wavelet_ft(wavelet, params, omega, scale):
+    """ContinuousWavelet.fourierTransform(omega, scale, 0) as a complex number."""
+    pr = _f64(list(params) + [0.0, 0.0])
+    re, im = ctypes.c_double(), ctypes.c_double()
+    lib().jwo_cwt_wavelet_ft_c(CWT_KINDS[wavelet] if isinstance(wavelet, str) else int(wavelet),
+                               _p(pr), ctypes.c_double(omega), ctypes.c_double(scale),
+                               ctypes.byref(re), ctypes.byref(im))
+    return complex(re.value, im.value)
+
+
 def cwt_fft(x, scales, fs=1.0, wavelet="morlet", params=(1.0, 1.0), padding=1, exact=False):
     """transformFFT restated; exact=True swaps the reference's recurrence twiddles for
     correctly rounded ones (the engine's choice) -- see jwo_set_exact_twiddles."""
     x, sc = _f64(x), _f64(scales)
-    pr = _f64(params)
+    pr = _f64(list(params) + [0.0, 0.0])
     n, ns = x.shape[0], sc.shape[0]
     out = np.empty((ns, n, 2))
     lib().jwo_set_exact_twiddles(1 if exact else 0)
     try:
-        lib().jwo_cwt_fft(0 if wavelet == "morlet" else 1, _p(pr), _p(x), ctypes.c_long(n),
+        lib().jwo_cwt_fft(CWT_KINDS[wavelet] if isinstance(wavelet, str) else int(wavelet),
+                          _p(pr), _p(x), ctypes.c_long(n),
                           _p(sc), ns, ctypes.c_double(fs), padding, _p(out))
     finally:
         lib().jwo_set_exact_twiddles(0)

@@ -189,6 +189,32 @@ def test_cwt_capi_rejects_bad_arguments():
     assert L.jw_cwt_fft(0, p, ptr(x), 0, ptr(sc[:1]), 1, 1.0, 1, ptr(out), 1, 0, None) == 0
 
 
+def test_cwt_capi_paul_dog_meyer_validation():
+    L = _native.lib()
+    x, sc, out = np.zeros(8), np.array([1.0]), np.zeros(2 * 8)
+    ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    cases = [(_native.JW_CWT_PAUL, (0.0, 0.0), "Order parameter m must be a positive integer"),
+             (_native.JW_CWT_PAUL, (2.5, 0.0), "Order parameter m must be a positive integer"),
+             (_native.JW_CWT_PAUL, (21.0, 0.0), "Order parameter m > 20 may cause numerical issues"),
+             (_native.JW_CWT_DOG, (0.0, 1.0), "Derivative order n must be a positive integer"),
+             (_native.JW_CWT_DOG, (11.0, 1.0), "Derivative order n > 10 may cause numerical issues"),
+             (_native.JW_CWT_DOG, (2.0, 0.0), "Width parameter sigma must be positive")]
+    for kind, prm, msg in cases:
+        p = (ctypes.c_double * 2)(*prm)
+        assert L.jw_cwt_fft(kind, p, ptr(x), 8, ptr(sc), 1, 1.0, 1, ptr(out), 1, 0, None) == -1
+        assert msg in _native.last_error(), (kind, prm)
+    neg = np.array([-1.0])
+    p = (ctypes.c_double * 2)(2.0, 1.0)
+    for kind in (_native.JW_CWT_DOG, _native.JW_CWT_MEYER):
+        assert L.jw_cwt_fft(kind, p, ptr(x), 8, ptr(neg), 1, 1.0, 1, ptr(out), 1, 0, None) == -1
+        assert "Scale must be positive" in _native.last_error()
+    # Meyer takes no parameters; empty input is a no-op for every kind
+    assert L.jw_cwt_fft(_native.JW_CWT_MEYER, None, ptr(x), 0, ptr(sc), 1, 1.0, 1, ptr(out), 1,
+                        0, None) == 0
+    assert L.jw_cwt_fft(_native.JW_CWT_MEYER + 1, p, ptr(x), 8, ptr(sc), 1, 1.0, 1, ptr(out), 1,
+                        0, None) == -1
+
+
 def test_cwt_result_accessors():
     from jwave.transforms import CWTResult
     c = np.array([[1 + 1j, -1 + 0j, 0j, -2 - 2j], [3 - 4j, 0 + 2j, -1 + 1e-300j, 1 - 1j]])

@@ -14,7 +14,8 @@ import pytest
 import oracle as orc
 from jwave import ContinuousWaveletTransform as CWT
 from jwave.transforms.cwt import PaddingType
-from jwave.transforms.wavelets.continuous import MexicanHatWavelet, MorletWavelet
+from jwave.transforms.wavelets.continuous import (DOGWavelet, MeyerWavelet, MexicanHatWavelet,
+                                                   MorletWavelet, PaulWavelet)
 
 pytestmark = pytest.mark.gpu
 
@@ -50,6 +51,29 @@ def test_small_lengths_all_paddings(n, padding):
 def test_mexican_hat(n):
     scales = CWT.generateLinearScales(0.5, 40.0, 6)
     check(MexicanHatWavelet(1.5), "mexhat", (1.5, 0.0), n, scales, PaddingType.SYMMETRIC)
+
+
+OTHERS = [(PaulWavelet(1), "paul", (1.0,)), (PaulWavelet(4), "paul", (4.0,)),
+          (PaulWavelet(20), "paul", (20.0,)),
+          (DOGWavelet(1, 2.0), "dog", (1.0, 2.0)), (DOGWavelet(2), "dog", (2.0, 1.0)),
+          (DOGWavelet(3, 0.5), "dog", (3.0, 0.5)), (DOGWavelet(4), "dog", (4.0, 1.0)),
+          (DOGWavelet(7, 1.3), "dog", (7.0, 1.3)), (MeyerWavelet(), "meyer", ())]
+
+
+@pytest.mark.parametrize("wv,kind,params", OTHERS, ids=lambda v: str(v)[:14])
+@pytest.mark.parametrize("n", [300, 4096, 1 << 17])
+def test_paul_dog_meyer(wv, kind, params, n):
+    # psi_hat real (Paul, even-n DOG) or complex (odd-n DOG, Meyer): X * conj(psi_hat)
+    scales = CWT.generateLogScales(0.5, 200.0, 5)
+    check(wv, kind, params, n, scales, PaddingType.PERIODIC, fs=1.7)
+
+
+def test_paul_negative_scale_not_rejected():
+    # PaulWavelet's fourierTransform(omega, scale, b) override has no scale check: the
+    # reference returns NaN columns (sqrt of a negative scale) rather than throwing
+    x = orc.fill_uniform(64, 3)
+    c = CWT(PaulWavelet(4)).transformFFT(x, np.array([-1.0, 2.0]), 1.0).getCoefficients()
+    assert np.all(np.isnan(c[0])) and np.all(np.isfinite(c[1]))
 
 
 @pytest.mark.parametrize("n", [1 << 13, 1 << 17, 1 << 18, 300001])
