@@ -28,6 +28,14 @@ namespace fast {
 #endif
 constexpr int kC = 512;           // samples per level per step (both directions)
 constexpr int kOOB = 0x7ffff000;  // byte offset beyond any row (N < 2^27): store dropped
+#ifndef JW_NT_ROWS
+#define JW_NT_ROWS 1
+#endif
+constexpr bool kNtRows = JW_NT_ROWS;
+#ifndef JW_INV_NT
+#define JW_INV_NT 0
+#endif
+constexpr bool kInvNt = JW_INV_NT;  // A/B builds: non-temporal coefficient loads (LDS-top inverse)
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef double d2 __attribute__((ext_vector_type(2)));
@@ -38,6 +46,10 @@ __device__ __forceinline__ rsrc_t make_rsrc(const double* p, long n) {
 }
 __device__ __forceinline__ double bload(rsrc_t r, int off) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+// non-temporal (streamed once): gives the line up early so rows that are re-read stay in L2
+__device__ __forceinline__ double bload_nt(rsrc_t r, int off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 2));
 }
 __device__ __forceinline__ void bstore(rsrc_t r, int off, double v) {
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, 0);
@@ -62,12 +74,15 @@ struct Geo {
   static constexpr int fwd_total = H + J * kC;  // doubles
 };
 
-// Inverse layout: VW_j = [C | hist_j] of (V_j, W_j) pairs, C samples per step.
-template <int L, int J, int C>
+// Inverse layout: VW_j = [C | hist_j] of (V_j, W_j) pairs, C samples per step.  With TOPG
+// the top level J is not staged in LDS at all (its taps are read from global memory, see
+// inv_step), so only levels 1..J-1 take space.
+template <int L, int J, int C, bool TOPG = false>
 struct GeoI {
   static constexpr int H = Geo<L, J>::H;
   static constexpr int inv_off(int j) { return Geo<L, J>::hoff(j) + (j - 1) * C; }  // pairs
-  static constexpr int inv_total = 2 * (H + J * C);                                  // doubles
+  static constexpr int inv_total =
+      TOPG ? 2 * (Geo<L, J>::hoff(J) + (J - 1) * C) : 2 * (H + J * C);  // doubles
 };
 
 // Flat history index e in [0, H) -> level j (1-based).
@@ -252,11 +267,12 @@ __device__ __forceinline__ int ring_idx(int j, const int (&rb)[J + 1], int ub, i
   return x + lane;
 }
 
-template <int L, int J, bool FMA, int C, int NT, int RF, class Fetch>
+template <int L, int J, bool FMA, int C, int NT, int RF, bool TOPG, class Fetch, class TapLoad>
 __device__ __forceinline__ void inv_step(d2* vw, double (&cur)[(C / NT) * (J + 1)],
                                          Fetch&& fetch, long a, long P, long seg_end,
-                                         const rsrc_t& rx, const Taps& taps, int (&rb)[J + 1]) {
-  using G = GeoI<L, J, C>;
+                                         const rsrc_t& rx, const Taps& taps, int (&rb)[J + 1],
+                                         double (&tv)[(C / NT) * 2 * L], TapLoad&& load_taps) {
+  using G = GeoI<L, J, C, TOPG>;
   using Rg = Ring<L, J, C, RF>;
   constexpr int R = C / NT;
   const int t = threadIdx.x;
@@ -269,16 +285,9 @@ __device__ __forceinline__ void inv_step(d2* vw, double (&cur)[(C / NT) * (J + 1
   auto ridx = [&](int j, int ubase, int u) {  // u = ubase + lane; non-ring levels use u as is
     return Rg::on(j) ? ring_idx<L, J, C, RF>(j, rb, ubase, lane) : u;
   };
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    vw[G::inv_off(J) + ridx(J, w64 + r * NT, t + r * NT)] =
-        d2{cur[(J + 1) * r + J], cur[(J + 1) * r + J - 1]};
-#pragma unroll
-    for (int j = 1; j < J; ++j) wj[r][j] = cur[(J + 1) * r + j - 1];
-  }
   // Inline history shift of linear level jj (see Ring::inline_shift).
   auto shift_level = [&](int jj) {
-    if (jj < 1 || jj > J || Rg::on(jj)) return;
+    if (jj < 1 || jj > J || Rg::on(jj) || (TOPG && jj == J)) return;
     const int hj = Geo<L, J>::hist(jj);
 #pragma unroll
     for (int e0 = 0; e0 < C; e0 += NT) {
@@ -287,11 +296,46 @@ __device__ __forceinline__ void inv_step(d2* vw, double (&cur)[(C / NT) * (J + 1
     }
   };
   constexpr bool kInline = Rg::inline_shift();
-  if constexpr (kInline) shift_level(1);  // level 1's chunk of the previous step
+  // Level 1's chunk of the previous step becomes history first: with TOPG and J = 2 the
+  // write below replaces that chunk (each lane shifts only slots it then rewrites itself).
+  if constexpr (kInline) shift_level(1);
+  if constexpr (TOPG) {
+    // Level J straight from registers: tap m = 0 is this lane's own sample of the chunk,
+    // taps m >= 1 were loaded from global memory (L2) one step ago by load_taps.  Same
+    // sums in the same order as the LDS path.
+    static_assert(J >= 2, "TOPG: at least two levels");
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const double* c = cur + (J + 1) * r;
+      const double* v = tv + 2 * L * r;
+#pragma unroll
+      for (int j = 1; j < J; ++j) wj[r][j] = c[j - 1];
+      double ap = madd<FMA>(0.0, taps.a[0], c[J]);
+      double dp = madd<FMA>(0.0, taps.b[0], c[J - 1]);
+#pragma unroll
+      for (int m = 1; m < L; ++m) {
+        ap = madd<FMA>(ap, taps.a[m], v[m]);
+        dp = madd<FMA>(dp, taps.b[m], v[L + m]);
+      }
+      vw[G::inv_off(J - 1) + ridx(J - 1, w64 + r * NT, t + r * NT)] = d2{ap + dp, wj[r][J - 1]};
+    }
+    load_taps();  // the next step's level-J taps: issued before this step's chunk fetch
+    // keep every tap load strictly older than the fetch (vmcnt counts in issue order: a tap
+    // load scheduled behind the fetch would make the next step wait for the fetch too)
+    __builtin_amdgcn_sched_barrier(0);
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      vw[G::inv_off(J) + ridx(J, w64 + r * NT, t + r * NT)] =
+          d2{cur[(J + 1) * r + J], cur[(J + 1) * r + J - 1]};
+#pragma unroll
+      for (int j = 1; j < J; ++j) wj[r][j] = cur[(J + 1) * r + j - 1];
+    }
+  }
   fetch(cur);  // the chunk two steps ahead
   JW_INV_SYNC();
 #pragma unroll
-  for (int j = J; j >= 1; --j) {
+  for (int j = TOPG ? J - 1 : J; j >= 1; --j) {
     const int d = 1 << (j - 1);
     const d2* src = vw + G::inv_off(j);
     if constexpr (kInline) shift_level(j + 1);
@@ -317,7 +361,9 @@ __device__ __forceinline__ void inv_step(d2* vw, double (&cur)[(C / NT) * (J + 1
   }
   // History shift of the linear levels: [0 .. hist_j) -> [C .. C + hist_j) (flat e over
   // their pairs: src e + (j-1)*C, dst e + j*C).
-  constexpr int HS = kInline ? 0 : Rg::shifted();
+  constexpr int HS = kInline ? 0
+                     : TOPG && Rg::shifted() > Geo<L, J>::hoff(J) ? Geo<L, J>::hoff(J)
+                                                                   : Rg::shifted();
   constexpr int kPer = (HS + NT - 1) / NT;
   if constexpr (kPer > 0) {
     d2 hv[kPer];
@@ -342,13 +388,18 @@ __device__ __forceinline__ void inv_step(d2* vw, double (&cur)[(C / NT) * (J + 1
   }
 }
 
-template <int L, int J, bool FMA, int C, int NT, int D, int RF>
-__global__ __launch_bounds__(NT) void modwt_inv_fast(const double* __restrict__ coeffs,
-                                                     double* __restrict__ x, long N,
-                                                     long seg_len, long a_start, long npairs,
-                                                     Taps taps) {
+// TOPG: level J's taps come from global memory (they were streamed through L2 a step or
+// more before; the other rows load non-temporal so these stay), so VW_J leaves LDS: 43 KB
+// instead of 61 KB for db4 J=8 (three workgroups per CU instead of two) and one barrier
+// phase fewer per step.  MINW = minimum waves per SIMD the register allocation must allow
+// (3 workgroups of 256 threads -> 3).
+template <int L, int J, bool FMA, int C, int NT, int D, int RF, bool TOPG, int MINW>
+__global__ __launch_bounds__(NT, MINW) void modwt_inv_fast(const double* __restrict__ coeffs,
+                                                           double* __restrict__ x, long N,
+                                                           long seg_len, long a_start,
+                                                           long npairs, Taps taps) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  using G = GeoI<L, J, C>;
+  using G = GeoI<L, J, C, TOPG>;
   constexpr int R = C / NT;
   const int t = threadIdx.x;
   const long P = (long)blockIdx.x * seg_len;
@@ -362,6 +413,7 @@ __global__ __launch_bounds__(NT) void modwt_inv_fast(const double* __restrict__ 
 
   long a = P + a_start;  // rightmost chunk start (segment end + warm-up, chunk aligned)
   long lb = a % N;
+  long lt = lb;  // TOPG: chunk start (mod N) of the step whose level-J taps load next
   auto fetch = [&](double (&dst)[R * (J + 1)]) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -369,21 +421,61 @@ __global__ __launch_bounds__(NT) void modwt_inv_fast(const double* __restrict__ 
       p = p >= N ? p - N : p;
       const int off = (int)(p * 8);
 #pragma unroll
-      for (int j = 0; j <= J; ++j) dst[(J + 1) * r + j] = bload(rc[j], off);
+      for (int j = 0; j <= J; ++j) {
+        // TOPG re-reads rows J-1 (W_J) and J (V_J) from L2 for the taps: stream the others
+        const bool nt = TOPG ? kNtRows && j < J - 1 : kInvNt;
+        dst[(J + 1) * r + j] = nt ? bload_nt(rc[j], off) : bload(rc[j], off);
+      }
     }
     lb -= C;
     if (lb < 0) lb += N;
   };
+  // Level-J taps m = 1..L-1 of one step: positions lt + t + m*2^(J-1) mod N.  Byte offsets
+  // stay below 2N*8 < 2^31, so the wrap is one unsigned min (o - N*8 wraps high when o < N*8);
+  // the dilation 2^(J-1) <= 512 <= N keeps every step below 2N.
+  double tv[R * 2 * L];
+  auto load_taps = [&]() {
+    if constexpr (TOPG) {
+      const unsigned n8 = (unsigned)(N * 8), d8 = 8u << (J - 1);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        unsigned o = (unsigned)((lt + t + r * NT) * 8);  // lt < N, t + r*NT < C <= N
+        o = min(o, o - n8);
+#pragma unroll
+        for (int m = 1; m < L; ++m) {
+          o += d8;
+          o = min(o, o - n8);
+          tv[2 * L * r + m] = bload(rc[J], (int)o);
+          tv[2 * L * r + L + m] = bload(rc[J - 1], (int)o);
+        }
+      }
+      lt -= C;
+      if (lt < 0) lt += N;
+    }
+  };
   // D register sets: the chunk of step s is fetched at the top of step s - D + ... so D-1
-  // whole steps of work hide each load.
+  // whole steps of work hide each load.  With TOPG the prologue issues, like the steady
+  // state, [set 0][stores][taps of step 0][set 1][stores], so the first step's counted wait
+  // matches the loop's.
   double S[D][R * (J + 1)];
 #pragma unroll
   for (int q = 0; q < D; ++q) {
+    if (TOPG && q == D - 1) {
+      load_taps();
+      __builtin_amdgcn_sched_barrier(0);
+    }
     fetch(S[q]);
     __builtin_amdgcn_sched_barrier(0);  // set q's loads strictly older than set q+1's
-  }
+    if constexpr (TOPG) {
 #pragma unroll
-  for (int i = 0; i < D * R; ++i) bstore(rx, kOOB - 8 * i, 0.0);  // queue-depth padding
+      for (int i = 0; i < R; ++i) bstore(rx, kOOB - 8 * (q * R + i), 0.0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if constexpr (!TOPG) {
+#pragma unroll
+    for (int i = 0; i < D * R; ++i) bstore(rx, kOOB - 8 * i, 0.0);  // queue-depth padding
+  }
   int rb[J + 1];
 #pragma unroll
   for (int j = 0; j <= J; ++j) rb[j] = 0;
@@ -391,7 +483,8 @@ __global__ __launch_bounds__(NT) void modwt_inv_fast(const double* __restrict__ 
   for (long k = 0; k < npairs; ++k) {  // npairs counts groups of D steps
 #pragma unroll
     for (int q = 0; q < D; ++q) {
-      inv_step<L, J, FMA, C, NT, RF>((d2*)lds, S[q], fetch, a, P, seg_end, rx, taps, rb);
+      inv_step<L, J, FMA, C, NT, RF, TOPG>((d2*)lds, S[q], fetch, a, P, seg_end, rx, taps, rb,
+                                           tv, load_taps);
       a -= C;
     }
   }
@@ -467,9 +560,9 @@ int launch_fwd(const Taps& t, const double* x, double* c, long N, int batch, hip
                 npairs, t);
 }
 
-template <int L, int J, bool FMA, int C, int D, int RF>
+template <int L, int J, bool FMA, int C, int NT, int D, int RF, bool TOPG = false>
 int launch_inv_c(const Taps& t, const double* c, double* x, long N, int batch, hipStream_t s) {
-  using G = GeoI<L, J, C>;
+  using G = GeoI<L, J, C, TOPG>;
   const long warm = ((long)(G::H + C - 1) / C) * C;
   const long seg = pick_seg(N, batch, warm, C);
   const long nseg = (N + seg - 1) / seg;
@@ -478,18 +571,41 @@ int launch_inv_c(const Taps& t, const double* c, double* x, long N, int batch, h
   const long a_start = (steps - 1) * C;  // surplus steps (to a multiple of D) run left of the segment
   const size_t lds = (size_t)G::inv_total * sizeof(double);
   const long cs = (long)(J + 1) * N;
-  return launch(modwt_inv_fast<L, J, FMA, C, C, D, RF>, lds, nseg, batch, C, s, c, cs, x, N, N, seg,
-                a_start, ngroups, t);
+  // workgroups of NT threads that fit a CU's 160 KB of LDS (at most 4: 16 waves of 256)
+  constexpr int kFit = (int)((160 * 1024) / ((size_t)G::inv_total * sizeof(double)));
+  constexpr int kMinW = (kFit < 1 ? 1 : kFit > 4 ? 4 : kFit) * NT / 256;
+  return launch(modwt_inv_fast<L, J, FMA, C, NT, D, RF, TOPG, (kMinW < 1 ? 1 : kMinW)>, lds, nseg,
+                batch, NT, s, c, cs, x, N, N, seg, a_start, ngroups, t);
 }
 
-// Inverse chunk C = 256 = threads per workgroup (one sample each per level; measured best
-// for db4 J=8: 2 workgroups per CU), two register sets.  The levels with dilation >= 64
-// (j >= 7) are ring buffers by default; env JW_INV_RING=off shifts every level (A/B runs).
+template <int L, int J, int C>
+constexpr bool inv_fits_topg() {
+  return J >= 2 && (size_t)GeoI<L, J, C, true>::inv_total * 8 <= 160 * 1024 &&
+         Geo<L, J>::H <= 16 * C;
+}
+
+// Inverse: two register sets; the levels with dilation >= 64 (j >= 7) are ring buffers by
+// default (env JW_INV_RING=off shifts every level, A/B runs).  Chunk C = 256 samples, one per
+// thread of 256.  A/B variants (measured equal on MI355X): env
+// JW_INV_TOP=global reads level J's taps from global memory (TOPG: 43 KB of LDS, three
+// workgroups per CU for db4 J=8) and JW_INV_C=512 then takes two samples per thread.
 template <int L, int J, bool FMA>
 int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hipStream_t s) {
+  constexpr int RF = J >= 7 ? 7 : J + 1;
   const char* e = std::getenv("JW_INV_RING");
-  if (e && e[0] == 'o') return launch_inv_c<L, J, FMA, 256, 2, J + 1>(t, c, x, N, batch, s);
-  return launch_inv_c<L, J, FMA, 256, 2, (J >= 7 ? 7 : J + 1)>(t, c, x, N, batch, s);
+  const char* top = std::getenv("JW_INV_TOP");
+  const char* ce = std::getenv("JW_INV_C");
+  const bool lds_top = !(top && top[0] == 'g');
+  const bool c512 = ce && ce[0] == '5';
+  if (e && e[0] == 'o') {
+    if (lds_top || J < 2) return launch_inv_c<L, J, FMA, 256, 256, 2, J + 1>(t, c, x, N, batch, s);
+    return launch_inv_c<L, J, FMA, 256, 256, 2, J + 1, (J >= 2)>(t, c, x, N, batch, s);
+  }
+  if (lds_top || J < 2) return launch_inv_c<L, J, FMA, 256, 256, 2, RF>(t, c, x, N, batch, s);
+  if constexpr (inv_fits_topg<L, J, 512>()) {
+    if (c512) return launch_inv_c<L, J, FMA, 512, 256, 2, RF, true>(t, c, x, N, batch, s);
+  }
+  return launch_inv_c<L, J, FMA, 256, 256, 2, RF, (J >= 2)>(t, c, x, N, batch, s);
 }
 
 // Returned when (L, J, N) has no fast kernel (the caller falls back to the generic ones).

@@ -74,18 +74,41 @@ def test_generic_kernels_bit_exact(wname, n, J, monkeypatch):
     assert bits_equal(m.inverseMODWT(ref), orc.modwt_inverse(ref, g, h, "direct_nz"))
 
 
+@pytest.mark.parametrize("top", ["global", "lds"])
 @pytest.mark.parametrize("ring", ["wave", "off"])
 @pytest.mark.parametrize("wname,n,J", [("Daubechies4", 70001, 8), ("Haar1", 50000, 10),
                                        ("Symlet8", 20000, 6), ("Daubechies2", 1000, 9),
                                        ("Daubechies8", 30001, 7), ("Daubechies10", 3000, 4),
-                                       ("Daubechies4", 1 << 16, 10)])
-def test_inverse_kernel_variants_bit_exact(wname, n, J, ring, monkeypatch):
+                                       ("Daubechies4", 1 << 16, 10), ("Daubechies4", 512, 8),
+                                       ("Daubechies20", 514, 2), ("Haar1", 600, 2)])
+def test_inverse_kernel_variants_bit_exact(wname, n, J, ring, top, monkeypatch):
     # JW_INV_RING=off shifts the history of every level instead of ring-buffering the levels
-    # with dilation >= 64; both must give the same bits
+    # with dilation >= 64; JW_INV_TOP=lds stages level J in LDS instead of reading its taps
+    # from global memory; every combination must give the same bits.  n = 512/514 with wide
+    # filters makes the level-J taps wrap around the signal more than once per step.
     wv = W.by_name(wname)
     g, h = ofilters(wv)
     c = orc.modwt_forward(orc.fill_uniform(n, 11 + n), J, g, h, "direct_nz")
     monkeypatch.setenv("JW_INV_RING", ring)
+    monkeypatch.setenv("JW_INV_TOP", top)
+    ref = orc.modwt_inverse(c, g, h, "direct_nz")
+    assert bits_equal(MODWTTransform(wv).inverseMODWT(c), ref)
+    xr = MODWTTransform(wv, arith="fma").inverseMODWT(c)
+    assert normwise(xr, ref) < FMA_TOL
+
+
+@pytest.mark.parametrize("chunk", ["256", "512"])
+@pytest.mark.parametrize("wname,n,J", [("Daubechies4", 70001, 8), ("Haar1", 50000, 10),
+                                       ("Symlet8", 20000, 6), ("Daubechies2", 1000, 9),
+                                       ("Daubechies4", 512, 8), ("Daubechies20", 514, 2),
+                                       ("Daubechies4", 1 << 16, 10), ("Haar1", 600, 2)])
+def test_inverse_chunk_variants_bit_exact(wname, n, J, chunk, monkeypatch):
+    # JW_INV_C=512: two samples per lane per level (level J from global memory)
+    wv = W.by_name(wname)
+    g, h = ofilters(wv)
+    c = orc.modwt_forward(orc.fill_uniform(n, 13 + n), J, g, h, "direct_nz")
+    monkeypatch.setenv("JW_INV_TOP", "global")
+    monkeypatch.setenv("JW_INV_C", chunk)
     ref = orc.modwt_inverse(c, g, h, "direct_nz")
     assert bits_equal(MODWTTransform(wv).inverseMODWT(c), ref)
     xr = MODWTTransform(wv, arith="fma").inverseMODWT(c)
