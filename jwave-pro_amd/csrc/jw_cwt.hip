@@ -15,8 +15,10 @@
 // through a group workspace A (G pairs x Np complex) that the Infinity Cache mostly absorbs;
 // the coefficients (B x ns x n complex) are written once -- that write is the roofline.
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <type_traits>
+#include <vector>
 
 #include "jw_fft_passes.hpp"
 
@@ -39,6 +41,7 @@ struct WaveletFT {
   int kind;        // JW_CWT_*
   int ord;         // Paul m, DOG n
   double p0, p1;   // Morlet (fb, fc); Mexican Hat and DOG (sigma, unused)
+  double p2;       // exponent factor: Morlet -2 pi^2 fb; Mexican Hat -0.5 sigma^2
   double norm;     // Morlet sqrt(2 pi fb); Mexican Hat ftNorm = nc sigma sqrt(2 pi);
                    // Paul and Meyer sqrt(2 pi); DOG sqrt(2 pi) sigma^(n+1)
   double norm2;    // DOG _normConstant (computeNormalizationConstant :357-366)
@@ -138,14 +141,36 @@ struct ScaleIn {  // X[sig][k] * conj(psi_hat(omega_k, a_s)), k = N2 k1 + col; i
   long N, N1, N2, pair0;
   int ns;
   double fs;
+  const double* sc;  // per scale (MORLET, MEXHAT): {bin step, norm * sqrt(a)}, see cwt_fft_device
   __device__ cplx operator()(long item, long k1, long col) const {
     const long p = pair0 + item, sig = p / ns;
     const int s = (int)(p - sig * ns);
     const long k = N2 * k1 + col;
-    double om = 2.0 * kPi * (double)k * fs / (double)N;  // createFrequencyAxis :453-456
-    if (k > N / 2) om -= 2.0 * kPi * fs;
-    const double a = scales[s];
-    const cplx wv = psi_hat<K>(w, om, a, sqrt(a));
+    cplx wv;
+    if constexpr (K == JW_CWT_MORLET || K == JW_CWT_MEXHAT) {
+      // The same spectra with the per-bin divisions hoisted into per-scale constants: the
+      // bin's signed index kk = k or k - N (createFrequencyAxis :453-456) times
+      //   Morlet:      f = a*omega/(2 pi) = kk * (a fs / N)            (MorletWavelet :114-124)
+      //   Mexican hat: a*omega = kk * (2 pi a fs / N)                  (MexicanHatWavelet :107-119)
+      // (a few ulps from the reference's operation order; the tests bound it at 1e-12).
+      const double kk = (double)(k > N / 2 ? k - N : k);
+      const double step = sc[2 * s], amp = sc[2 * s + 1];
+      double e, m = amp;
+      if constexpr (K == JW_CWT_MORLET) {
+        const double d = kk * step - w.p1;
+        e = w.p2 * d * d;  // p2 = -2 pi^2 fb
+      } else {
+        const double om = kk * step, om2 = om * om;
+        e = w.p2 * om2;  // p2 = -0.5 sigma^2
+        m *= om2;
+      }
+      wv = make_double2(e < -746.0 ? 0.0 : m * exp(e), 0.0);
+    } else {
+      double om = 2.0 * kPi * (double)k * fs / (double)N;  // createFrequencyAxis :453-456
+      if (k > N / 2) om -= 2.0 * kPi * fs;
+      const double a = scales[s];
+      wv = psi_hat<K>(w, om, a, sqrt(a));
+    }
     if (wv.x == 0.0 && wv.y == 0.0) return make_double2(0.0, 0.0);  // skip the X read
     const cplx xv = X[sig * N + col * N1 + k1];
     if constexpr (K == JW_CWT_DOG || K == JW_CWT_MEYER) {
@@ -220,12 +245,26 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   const long ws = (gmb ? std::atol(gmb) : 128L) << 20;
   const long per = std::max(1L, ws / (N * (long)sizeof(cplx)));
   const long gsig = std::min<long>(batch, per), gpair = std::min<long>((long)batch * ns, per);
+  // N = 2^18 (512 x 512): the pairs' inverse FFTs are software-pipelined over two workspaces
+  // (run_fft512_pipelined); env JW_CWT_PIPE=0 runs the groups one after the other (A/B runs).
+  const char* gpp = std::getenv("JW_CWT_PIPE");
+  const bool pipe = N == (1L << 18) && (long)batch * ns > gpair && !(gpp && gpp[0] == '0');
   cplx *X = nullptr, *A = nullptr;
   double* dsc = nullptr;
+  const long a_items = std::max(gsig, pipe ? 2 * gpair : gpair);
   JW_HIP_TRY(hipMallocAsync((void**)&X, (size_t)batch * N * sizeof(cplx), s));
-  JW_HIP_TRY(hipMallocAsync((void**)&A, (size_t)std::max(gsig, gpair) * N * sizeof(cplx), s));
-  JW_HIP_TRY(hipMallocAsync((void**)&dsc, (size_t)ns * sizeof(double), s));
-  JW_HIP_TRY(hipMemcpyAsync(dsc, scales_host, (size_t)ns * sizeof(double), hipMemcpyHostToDevice, s));
+  JW_HIP_TRY(hipMallocAsync((void**)&A, (size_t)a_items * N * sizeof(cplx), s));
+  // device scale table: [a_0 .. a_{ns-1} | (step, norm*sqrt(a)) per scale] (ScaleIn)
+  std::vector<double> hsc(3 * (size_t)ns);
+  for (int i = 0; i < ns; ++i) {
+    const double a = scales_host[i];
+    hsc[i] = a;
+    hsc[ns + 2 * i] = wavelet == JW_CWT_MEXHAT ? 2.0 * kPi * a * fs / (double)N : a * fs / (double)N;
+    hsc[ns + 2 * i + 1] = w.norm * std::sqrt(a);
+  }
+  w.p2 = wavelet == JW_CWT_MORLET ? -2.0 * kPi * kPi * w.p0 : -0.5 * w.p0 * w.p0;
+  JW_HIP_TRY(hipMallocAsync((void**)&dsc, hsc.size() * sizeof(double), s));
+  JW_HIP_TRY(hipMemcpyAsync(dsc, hsc.data(), hsc.size() * sizeof(double), hipMemcpyHostToDevice, s));
   int logN = 0;
   while ((1L << logN) < N) ++logN;
   const long N1 = N <= 4096 ? N : 1L << ((logN + 1) / 2);
@@ -238,12 +277,31 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   }
   // per (signal, scale) pair: IFFT(X * psi_hat) -> coefficients
   const long pairs = (long)batch * ns;
-  for (long p0 = 0; p0 < pairs && st == JW_OK; p0 += gpair) {
+  if (pipe && st == JW_OK) {
+    auto go = [&](auto kind) {
+      constexpr int K = decltype(kind)::value;
+      auto mk_in = [&](long p0) {
+        return ScaleIn<K>{X, dsc, w, N, N1, N / N1, p0, ns, fs, dsc + ns};
+      };
+      auto mk_out = [&](long p0) { return CoefOut{out, n, N1, p0, 1.0 / (double)N, (ntm & 2) != 0}; };
+      return fft::run_fft512_pipelined<1>(N, pairs, gpair, mk_in, mk_out, A, A + gpair * N, s, T,
+                                          (ntm & 1) != 0);
+    };
+    switch (wavelet) {
+      case JW_CWT_MORLET: st = go(std::integral_constant<int, JW_CWT_MORLET>{}); break;
+      case JW_CWT_MEXHAT: st = go(std::integral_constant<int, JW_CWT_MEXHAT>{}); break;
+      case JW_CWT_PAUL: st = go(std::integral_constant<int, JW_CWT_PAUL>{}); break;
+      case JW_CWT_DOG: st = go(std::integral_constant<int, JW_CWT_DOG>{}); break;
+      default: st = go(std::integral_constant<int, JW_CWT_MEYER>{}); break;
+    }
+  }
+  for (long p0 = 0; p0 < pairs && st == JW_OK && !pipe; p0 += gpair) {
     const long np_ = std::min<long>(gpair, pairs - p0);
     CoefOut o{out, n, N <= 4096 ? 1 : N1, p0, 1.0 / (double)N, (ntm & 2) != 0};
     CoefOut o1{out, n, 1, p0, 1.0 / (double)N, (ntm & 2) != 0};
     auto go = [&](auto kind) {
-      ScaleIn<decltype(kind)::value> in{X, dsc, w, N, N1, N <= 4096 ? 1 : N / N1, p0, ns, fs};
+      ScaleIn<decltype(kind)::value> in{X, dsc, w, N, N1, N <= 4096 ? 1 : N / N1, p0, ns, fs,
+                                        dsc + ns};
       return run_fft<1>(N, np_, in, o1, o, A, s, T, (ntm & 1) != 0);
     };
     switch (wavelet) {

@@ -28,11 +28,9 @@ static_assert(kTile >= kT * fft::kXbuf, "tile must hold the exchange buffers");
 // IN_TILE: the line's inputs are strided (pass 1 over a natural-order array): stage 8 lines
 // through the tile.  TWID: apply the four-step twiddle W_N^(S n1 col) (pass 1).
 template <int S, bool IN_TILE, bool TWID, class In, class Out>
-__global__ __launch_bounds__(512) void pass512(In in, Out out, long N, long N2, Tables T) {
-  __shared__ cplx tile[kTile];
+__device__ __forceinline__ void pass512_body(const In& in, const Out& out, long N, long N2,
+                                             const Tables& T, long item, long line0, cplx* tile) {
   const int tid = threadIdx.x, lane = tid & 63, c = tid >> 6;
-  const long item = blockIdx.y;
-  const long line0 = (long)blockIdx.x * kT;
   cplx a[8];
   if (IN_TILE) {
     // tile[k1][c] <- in(k1, line0 + c): 8 consecutive columns per row, coalesced
@@ -71,6 +69,49 @@ __global__ __launch_bounds__(512) void pass512(In in, Out out, long N, long N2, 
   for (int i = 0; i < 8; ++i) {
     const int n = (tid >> 3) + 64 * i, cc = tid & 7;
     out(item, n, line0 + cc, tile[n * (kT + 1) + cc]);
+  }
+}
+
+template <int S, bool IN_TILE, bool TWID, class In, class Out>
+__global__ __launch_bounds__(512) void pass512(In in, Out out, long N, long N2, Tables T) {
+  __shared__ cplx tile[kTile];
+  pass512_body<S, IN_TILE, TWID>(in, out, N, N2, T, blockIdx.y, (long)blockIdx.x * kT, tile);
+}
+
+// Two independent 512-line passes in one grid, for software pipelining of a batch of
+// four-step transforms: role 0 = pass 2 (rows) of group g, role 1 = pass 1 (columns) of
+// group g+1, each on its own workspace.  Pass 2 is HBM-bound and pass 1 mostly on-chip
+// (spectra from L2, psi_hat arithmetic), so interleaving their blocks on every CU overlaps
+// the two.  Blocks alternate roles while both have work left (so both spread over all CUs).
+struct TwoRoles {
+  long nb0, nb1;        // blocks of each role
+  long lines0, lines1;  // lines per item / kT (blocks per item)
+  __device__ void pick(long b, int& role, long& item, long& line0) const {
+    const long m = nb0 < nb1 ? nb0 : nb1;
+    long idx;
+    if (b < 2 * m) {
+      role = (int)(b & 1);
+      idx = b >> 1;
+    } else {
+      role = nb0 > nb1 ? 0 : 1;
+      idx = m + (b - 2 * m);
+    }
+    const long per = role == 0 ? lines0 : lines1;
+    item = idx / per;
+    line0 = (idx - item * per) * kT;
+  }
+};
+template <int S, class In0, class Out0, bool IT1, class In1, class Out1>
+__global__ __launch_bounds__(512) void pass512_two(In0 in0, Out0 out0, In1 in1, Out1 out1, long N,
+                                                   long N2, TwoRoles R, Tables T) {
+  __shared__ cplx tile[kTile];
+  int role;
+  long item, line0;
+  R.pick(blockIdx.x, role, item, line0);
+  if (role == 0) {
+    pass512_body<S, false, false>(in0, out0, N, N2, T, item, line0, tile);
+  } else {
+    pass512_body<S, IT1, true>(in1, out1, N, N2, T, item, line0, tile);
   }
 }
 
@@ -187,6 +228,43 @@ int run_fft(long N, long items, In1 in1, Out1 out_single, Out2 out_final, cplx* 
                        dim3(256), (size_t)N2 * sizeof(cplx), s, a_in, out_final, N, N2, log2, T);
   }
   JW_HIP_TRY(hipGetLastError());
+  return JW_OK;
+}
+
+// A batch of `items` four-step FFTs of N = 512 x 512 points, in groups of `gsize` items,
+// software-pipelined: one launch runs pass 2 of group g (workspace A[g % 2]) beside pass 1
+// of group g+1 (workspace A[(g+1) % 2]).  mk_in(p0) / mk_out(p0) build the input / final
+// output functors of the group whose first item is p0 (item indices inside a group are
+// relative to p0, as in run_fft).
+template <int S, class MkIn, class MkOut>
+int run_fft512_pipelined(long N, long items, long gsize, MkIn mk_in, MkOut mk_out, cplx* A0,
+                         cplx* A1, hipStream_t s, const Tables& T, bool a_nt) {
+  constexpr long N1 = 512, N2 = 512;
+  if (N != N1 * N2) return fail(JW_ERR_UNSUPPORTED, "pipelined FFT needs N = 2^18");
+  using In1 = decltype(mk_in(0L));
+  using Out2 = decltype(mk_out(0L));
+  cplx* A[2] = {A0, A1};
+  const long G = (items + gsize - 1) / gsize;
+  auto cnt = [&](long g) { return items - g * gsize < gsize ? items - g * gsize : gsize; };
+  hipLaunchKernelGGL((pass512<S, In1::kStrided, true, In1, ColOut>),
+                     dim3((unsigned)(N2 / kT), (unsigned)cnt(0)), dim3(512), 0, s, mk_in(0L),
+                     ColOut{A[0], N, N2, a_nt}, N, N2, T);
+  JW_HIP_TRY(hipGetLastError());
+  for (long g = 1; g <= G; ++g) {
+    const RowIn rin{A[(g - 1) & 1], N, N2};
+    if (g == G) {
+      hipLaunchKernelGGL((pass512<S, false, false, RowIn, Out2>),
+                         dim3((unsigned)(N1 / kT), (unsigned)cnt(g - 1)), dim3(512), 0, s, rin,
+                         mk_out((g - 1) * gsize), N, N2, T);
+    } else {
+      const TwoRoles R{(N1 / kT) * cnt(g - 1), (N2 / kT) * cnt(g), N1 / kT, N2 / kT};
+      hipLaunchKernelGGL((pass512_two<S, RowIn, Out2, In1::kStrided, In1, ColOut>),
+                         dim3((unsigned)(R.nb0 + R.nb1)), dim3(512), 0, s, rin,
+                         mk_out((g - 1) * gsize), mk_in(g * gsize), ColOut{A[g & 1], N, N2, a_nt},
+                         N, N2, R, T);
+    }
+    JW_HIP_TRY(hipGetLastError());
+  }
   return JW_OK;
 }
 

@@ -100,6 +100,28 @@ def test_batch_and_device_tensors(device):
         assert nw(host[b], ex) < TOL_EXACT
 
 
+@pytest.mark.parametrize("kind", ["morlet", "mexhat", "dog"])
+def test_pipelined_groups_bit_identical(kind, monkeypatch):
+    # N = 2^18 runs the (signal, scale) inverse FFTs in groups, pass 2 of one group beside
+    # pass 1 of the next; an 8 MiB workspace makes groups of 2 pairs (7 groups, last one
+    # short).  The pipelined and sequential schedules do the same arithmetic: equal bits.
+    n, B = 1 << 18, 2
+    scales = CWT.generateLogScales(2.0, 1024.0, 7)
+    xs = np.stack([orc.fill_uniform(n, 21 + b) for b in range(B)])
+    wv, params = {"morlet": (MorletWavelet(*MORLET6), MORLET6),
+                  "mexhat": (MexicanHatWavelet(1.5), (1.5, 0.0)),
+                  "dog": (DOGWavelet(3, 0.5), (3.0, 0.5))}[kind]
+    monkeypatch.setenv("JW_CWT_GROUP_MB", "8")
+    monkeypatch.setenv("JW_CWT_PIPE", "1")
+    piped = CWT(wv).transformFFTBatch(xs, scales)
+    monkeypatch.setenv("JW_CWT_PIPE", "0")
+    seq = CWT(wv).transformFFTBatch(xs, scales)
+    assert np.array_equal(piped, seq)
+    for b in range(B):
+        ex = orc.cwt_fft(xs[b], scales, 1.0, kind, params, 1, exact=True)
+        assert nw(piped[b], ex) < TOL_EXACT
+
+
 def test_sinusoid_peaks_at_matching_scale():
     # Morlet with fc = 6/(2 pi): scale a resonates with frequency fc / a (scaleToFrequency)
     n, fs = 1 << 14, 1.0
