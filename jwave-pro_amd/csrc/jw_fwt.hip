@@ -218,10 +218,10 @@ __device__ __forceinline__ d2 rev_pair_wrapped(const double* buf, int h, int u,
 
 // The forward cascade on one line held in LDS (buf), by NTL threads (tid < NTL).  The
 // barriers are workgroup-wide: every line of the workgroup runs the same levels.
-template <bool FMA, int M, int NTL>
+template <bool FMA, int M, int NTL, int LEN = kLdsN>
 __device__ __forceinline__ void cascade_fwd(double* buf, int n, int level, int tw, int tid,
                                             const Filters& f) {
-  constexpr int P = kLdsN / NTL / 2;  // pairs per thread at the first level (max)
+  constexpr int P = (LEN / NTL / 2) < 1 ? 1 : LEN / NTL / 2;  // pairs per thread, first level
   int l = 0;
   for (int h = n; h >= tw && h >= 2 && l < level; h >>= 1, ++l) {
     const int half = h >> 1, mask = h - 1;
@@ -270,10 +270,10 @@ __global__ __launch_bounds__(kNT2) void fwt_fwd_lds2(const double* __restrict__ 
   for (int i = 2 * tid; i < n; i += 2 * kNT2) *(d2*)&ys[i] = *(const d2*)&buf[i];
 }
 
-template <bool FMA, int M, int KIND, int NTL>
+template <bool FMA, int M, int KIND, int NTL, int LEN = kLdsN>
 __device__ __forceinline__ void cascade_rev(double* buf, int n, int h0, int tw, int tid,
                                             const Filters& f) {
-  constexpr int P = kLdsN / NTL / 2;
+  constexpr int P = (LEN / NTL / 2) < 1 ? 1 : LEN / NTL / 2;
   for (int h = h0; h <= n && h >= tw && h >= 2; h <<= 1) {
     const int half = h >> 1;
     // pairs u < nslow see wrapped taps: all of them when h < M, else the first M/2 - 1; they
@@ -503,6 +503,144 @@ __global__ __launch_bounds__(NL * 256) void fwt_lines4(const double* in,
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// 2-D column pass for tall matrices (rows > the tail length): the first S levels of every
+// column run as "strip" kernels that work on whole row segments -- a workgroup owns kSW = 64
+// columns (512-byte row pieces, fully coalesced) and kST output rows of one level, staged
+// through LDS -- and the remaining levels run on the top rows >> S rows with the LDS
+// cascade, kTailNL columns per workgroup (fwt_cols_tail).  Same sums, same order as
+// Wavelet.forward/reverse per column (bit-identical in STRICT).
+// ---------------------------------------------------------------------------------------
+constexpr int kSW = 64;      // columns per strip workgroup (32 lanes x 2 columns)
+constexpr int kST = 32;      // output rows per strip workgroup
+constexpr int kTailNL = 16;  // columns per tail workgroup (128-byte row pieces)
+constexpr int kTailLen = 1024;
+
+struct Strip {  // one level's buffers, each [rows][cols] per matrix with its own matrix stride
+  const double* src;  // forward: level input rows [0, h); reverse: approximations rows [0, h/2)
+  const double* srcd; // reverse: details rows [0, h/2)
+  double* dsta;       // forward: approximations rows [0, h/2); reverse: output rows [0, h)
+  double* dstd;       // forward: details rows [0, h/2)
+  long ms_src, ms_srcd, ms_dsta, ms_dstd;
+  int cols, h;
+};
+
+// Forward level on rows [0, h) of every column: approximation row i -> dsta, detail -> dstd.
+template <bool FMA, int M>
+__global__ __launch_bounds__(256) void fwt_strip_fwd(Strip s, Filters f) {
+  constexpr int NR = 2 * kST + M - 2;  // input rows of one strip
+  __shared__ __attribute__((aligned(16))) double tile[NR * kSW];
+  const int tid = threadIdx.x, cp = tid & 31, rl = tid >> 5;
+  const int nchunk = s.cols / kSW;
+  const int chunk = blockIdx.x % nchunk, strip = blockIdx.x / nchunk;
+  const long mat = blockIdx.y;
+  const int c0 = chunk * kSW, i0 = strip * kST, mask = s.h - 1;
+  const double* src = s.src + mat * s.ms_src + c0;
+  for (int r = rl; r < NR; r += 8) {
+    const int row = (2 * i0 + r) & mask;  // (2i + j) mod h, h a power of two
+    *(d2*)&tile[r * kSW + 2 * cp] = *(const d2*)&src[(long)row * s.cols + 2 * cp];
+  }
+  __syncthreads();
+  double* da = s.dsta + mat * s.ms_dsta + c0 + 2 * cp;
+  double* dd = s.dstd + mat * s.ms_dstd + c0 + 2 * cp;
+#pragma unroll
+  for (int q = 0; q < kST / 8; ++q) {
+    const int i = rl + 8 * q;
+    double l0 = 0., l1 = 0., h0 = 0., h1 = 0.;
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      const d2 v = *(const d2*)&tile[(2 * i + j) * kSW + 2 * cp];
+      l0 = madd<FMA>(l0, f.sD[j], v.x);
+      h0 = madd<FMA>(h0, f.wD[j], v.x);
+      l1 = madd<FMA>(l1, f.sD[j], v.y);
+      h1 = madd<FMA>(h1, f.wD[j], v.y);
+    }
+    *(d2*)&da[(long)(i0 + i) * s.cols] = d2{l0, l1};
+    *(d2*)&dd[(long)(i0 + i) * s.cols] = d2{h0, h1};
+  }
+}
+
+// Reverse level: output rows [0, h) from approximations a and details d (rows [0, h/2) each),
+// Wavelet.reverse's scatter gathered per output in the scatter's order: output pair
+// (2u, 2u+1) adds the taps t (i = u - t mod h/2) by t descending, except that the outputs
+// whose taps wrap (u < M/2 - 1) add the unwrapped i first, i ascending, then the wrapped i
+// (near h/2), i ascending: t = u, ..., 0, M/2 - 1, ..., u + 1.  Needs h/2 >= M.
+template <bool FMA, int M, int KIND>
+__global__ __launch_bounds__(256) void fwt_strip_rev(Strip s, Filters f) {
+  constexpr int T2 = M / 2;
+  constexpr int NI = kST / 2 + T2 - 1;  // a/d rows of one strip
+  __shared__ __attribute__((aligned(16))) double ta[NI * kSW], td[NI * kSW];
+  const int tid = threadIdx.x, cp = tid & 31, rl = tid >> 5;
+  const int nchunk = s.cols / kSW;
+  const int chunk = blockIdx.x % nchunk, strip = blockIdx.x / nchunk;
+  const long mat = blockIdx.y;
+  const int c0 = chunk * kSW, k0 = strip * kST, half = s.h >> 1;
+  const int ibase = k0 / 2 - (T2 - 1);  // tile row r holds i = ibase + r (mod h/2)
+  const double* sa = s.src + mat * s.ms_src + c0;
+  const double* sd = s.srcd + mat * s.ms_srcd + c0;
+  for (int r = rl; r < NI; r += 8) {
+    const int row = (ibase + r) & (half - 1);
+    *(d2*)&ta[r * kSW + 2 * cp] = *(const d2*)&sa[(long)row * s.cols + 2 * cp];
+    *(d2*)&td[r * kSW + 2 * cp] = *(const d2*)&sd[(long)row * s.cols + 2 * cp];
+  }
+  __syncthreads();
+  double* dst = s.dsta + mat * s.ms_dsta + c0 + 2 * cp;
+#pragma unroll
+  for (int q = 0; q < kST / 16; ++q) {
+    const int ul = rl + 8 * q;  // local output pair: rows k0 + 2ul, k0 + 2ul + 1
+    const int u = k0 / 2 + ul;
+    const int tstart = u >= T2 - 1 ? T2 - 1 : u;
+    double e0 = 0., e1 = 0., o0 = 0., o1 = 0.;  // (even, odd row) x (column 0, column 1)
+#pragma unroll
+    for (int tt = 0; tt < T2; ++tt) {
+      int t = tstart - tt;
+      t = t < 0 ? t + T2 : t;
+      const int r = ul + (T2 - 1) - t;  // tile row of i = u - t
+      const d2 av = *(const d2*)&ta[r * kSW + 2 * cp];
+      const d2 dv = *(const d2*)&td[r * kSW + 2 * cp];
+      const double sr0 = f.sR[2 * t], wr0 = f.wR[2 * t], sr1 = f.sR[2 * t + 1], wr1 = f.wR[2 * t + 1];
+      e0 += contrib<FMA>(av.x, dv.x, sr0, wr0, KIND);
+      e1 += contrib<FMA>(av.y, dv.y, sr0, wr0, KIND);
+      o0 += contrib<FMA>(av.x, dv.x, sr1, wr1, KIND);
+      o1 += contrib<FMA>(av.y, dv.y, sr1, wr1, KIND);
+    }
+    *(d2*)&dst[(long)(k0 + 2 * ul) * s.cols] = d2{e0, e1};
+    *(d2*)&dst[(long)(k0 + 2 * ul + 1) * s.cols] = d2{o0, o1};
+  }
+}
+
+// The remaining levels of kTailNL columns on rows [0, len) (len <= kTailLen), in LDS:
+// forward levels lvl_h0 = level count from h = len; reverse from h = lvl_h0 up to len.
+template <bool FMA, int M, bool REV, int KIND>
+__global__ __launch_bounds__(1024) void fwt_cols_tail(const double* in, double* out, int len,
+                                                      int cols, long ms_in, long ms_out,
+                                                      int lvl_h0, int tw, Filters f) {
+  constexpr int NTL = 1024 / kTailNL;
+  constexpr int PAD = kTailLen + 2;  // 16-byte aligned lines; the transposed stores spread banks
+  __shared__ __attribute__((aligned(16))) double bufs[kTailNL * PAD];
+  const int tid = threadIdx.x, g = tid / NTL, lt = tid % NTL;
+  const int nchunk = cols / kTailNL;
+  const long mat = blockIdx.x / nchunk;
+  const int line0 = (int)(blockIdx.x % nchunk) * kTailNL;
+  const double* src = in + mat * ms_in + line0;
+  double* dst = out + mat * ms_out + line0;
+  for (int k = tid; k < len * kTailNL; k += 1024) {
+    const int i = k / kTailNL, c = k % kTailNL;
+    bufs[c * PAD + i] = src[(long)i * cols + c];
+  }
+  __syncthreads();
+  double* buf = bufs + g * PAD;
+  if (REV) {
+    cascade_rev<FMA, M, KIND, NTL, kTailLen>(buf, len, lvl_h0, tw, lt, f);
+  } else {
+    cascade_fwd<FMA, M, NTL, kTailLen>(buf, len, lvl_h0, tw, lt, f);
+  }
+  for (int k = tid; k < len * kTailNL; k += 1024) {
+    const int i = k / kTailNL, c = k % kTailNL;
+    dst[(long)i * cols + c] = bufs[c * PAD + i];
+  }
+}
+
 // One level on global memory (long signals): out[0..h) of every signal from in[0..h).
 template <bool FMA>
 __global__ __launch_bounds__(kNT) void fwt_fwd_level(const double* __restrict__ in,
@@ -624,6 +762,56 @@ bool launch_cols(int M, int kind, bool rev, hipStream_t s, const double* in, dou
   if (e ? e[0] == '2' : rev)
     return launch_cols_nl<FMA, 2>(M, kind, rev, s, in, out, rows, cols, lvl_h0, tw, batch, f);
   return launch_cols_nl<FMA, 4>(M, kind, rev, s, in, out, rows, cols, lvl_h0, tw, batch, f);
+}
+
+// Strip / tail column kernels (filter lengths with compiled instances).
+#define JW_STRIP_LENGTHS(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20)
+
+template <bool FMA>
+bool launch_strip(int M, int kind, bool rev, hipStream_t s, const Strip& st, int batch,
+                  const Filters& f) {
+  const int rows_out = rev ? st.h : st.h / 2;  // output rows of the level (per kind of output)
+  const dim3 g((unsigned)((st.cols / kSW) * (rows_out / kST)), (unsigned)batch), b(256);
+  switch (M) {
+#define JW_C(MM)                                                                              \
+  case MM:                                                                                    \
+    if (!rev)                                                                                 \
+      hipLaunchKernelGGL((fwt_strip_fwd<FMA, MM>), g, b, 0, s, st, f);                        \
+    else if (kind == JW_WAVELET_HAAR_ORTH)                                                    \
+      hipLaunchKernelGGL((fwt_strip_rev<FMA, MM, JW_WAVELET_HAAR_ORTH>), g, b, 0, s, st, f);  \
+    else                                                                                      \
+      hipLaunchKernelGGL((fwt_strip_rev<FMA, MM, JW_WAVELET_GENERIC>), g, b, 0, s, st, f);    \
+    return true;
+    JW_STRIP_LENGTHS(JW_C)
+#undef JW_C
+    default:
+      return false;
+  }
+}
+
+template <bool FMA>
+bool launch_tail(int M, int kind, bool rev, hipStream_t s, const double* in, double* out, int len,
+                 int cols, long ms_in, long ms_out, int lvl_h0, int tw, int batch,
+                 const Filters& f) {
+  const dim3 g((unsigned)((long)batch * (cols / kTailNL))), b(1024);
+  switch (M) {
+#define JW_C(MM)                                                                                \
+  case MM:                                                                                      \
+    if (!rev)                                                                                   \
+      hipLaunchKernelGGL((fwt_cols_tail<FMA, MM, false, 0>), g, b, 0, s, in, out, len, cols,     \
+                         ms_in, ms_out, lvl_h0, tw, f);                                         \
+    else if (kind == JW_WAVELET_HAAR_ORTH)                                                      \
+      hipLaunchKernelGGL((fwt_cols_tail<FMA, MM, true, JW_WAVELET_HAAR_ORTH>), g, b, 0, s, in,   \
+                         out, len, cols, ms_in, ms_out, lvl_h0, tw, f);                         \
+    else                                                                                        \
+      hipLaunchKernelGGL((fwt_cols_tail<FMA, MM, true, JW_WAVELET_GENERIC>), g, b, 0, s, in, out, \
+                         len, cols, ms_in, ms_out, lvl_h0, tw, f);                              \
+    return true;
+    JW_STRIP_LENGTHS(JW_C)
+#undef JW_C
+    default:
+      return false;
+  }
 }
 
 Filters make_filters(const FwtPlan& p) {
@@ -827,12 +1015,110 @@ int wpt_reverse_device(const FwtPlan& p, const double* y, double* x, long n, int
                                  : wpt_t<false>(p, true, y, x, n, level, batch, s);
 }
 
+// Column levels that run as strips for a [rows][cols] 2-D pass (0: use fwt_lines4).  Strips
+// run while h > the tail length (env JW_FWT_TAIL overrides it, for tests; JW_FWT_STRIP=0
+// disables the strips).  Transform wavelength 2 keeps the reverse's first level at
+// rows >> (lvlM - 1) (FastWaveletTransform.java:137-141).
+int strip_levels(const FwtPlan& p, int rows, int cols, int lvlM) {
+  const char* e = std::getenv("JW_FWT_STRIP");
+  if ((e && e[0] == '0') || std::getenv("JW_FWT_GENERIC")) return 0;
+  if (p.M % 2 || p.M > 20 || p.tw != 2 || cols % kSW || cols > kLdsN || (rows & (rows - 1)))
+    return 0;
+  const char* te = std::getenv("JW_FWT_TAIL");
+  long tail = te ? std::atol(te) : kTailLen;
+  if (tail > kTailLen) tail = kTailLen;
+  if (tail < 2 * kST) tail = 2 * kST;
+  int S = 0;
+  long h = rows;
+  while (S < lvlM && h > tail && h / 2 >= p.M) {
+    ++S;
+    h >>= 1;
+  }
+  if (S < lvlM && h > kTailLen) return 0;  // the remaining levels would not fit the tail
+  return S;
+}
+
+template <bool FMA>
+int fwt2d_forward_strips(const FwtPlan& p, int S, const double* x, double* y, int rows, int cols,
+                         int lvlM, int lvlN, int batch, hipStream_t s) {
+  const long mat = (long)rows * cols, half = mat / 2;
+  double *T = nullptr, *B = nullptr;
+  JW_HIP_TRY(hipMallocAsync((void**)&T, sizeof(double) * mat * batch, s));
+  JW_HIP_TRY(hipMallocAsync((void**)&B, sizeof(double) * half * batch, s));
+  int st = fwt_forward_device(p, x, T, cols, lvlN, rows * batch, s);  // rows -> T
+  const Filters f = make_filters(p);
+  const int tail_lv = lvlM - S;
+  double* bufs[2] = {T, B};
+  const long ms[2] = {mat, half};
+  int cur = 0;  // buffer holding the current level's input (approximations)
+  for (int l = 0; l < S && st == JW_OK; ++l) {
+    const int h = rows >> l;
+    const bool to_y = l == S - 1 && tail_lv == 0;
+    const Strip sp{bufs[cur], nullptr, to_y ? y : bufs[cur ^ 1], y + (long)(h / 2) * cols,
+                   ms[cur], 0, to_y ? mat : ms[cur ^ 1], mat, cols, h};
+    if (!launch_strip<FMA>(p.M, p.kind, false, s, sp, batch, f)) st = fail(JW_ERR_UNSUPPORTED, "no 2-D strip kernel for filter length %d", p.M);
+    cur ^= 1;
+  }
+  if (st == JW_OK && tail_lv > 0 &&
+      !launch_tail<FMA>(p.M, p.kind, false, s, bufs[cur], y, rows >> S, cols, ms[cur], mat, tail_lv,
+                        p.tw, batch, f))
+    st = fail(JW_ERR_UNSUPPORTED, "no 2-D strip kernel for filter length %d", p.M);
+  if (st == JW_OK) JW_HIP_TRY(hipGetLastError());
+  (void)hipFreeAsync(B, s);
+  (void)hipFreeAsync(T, s);
+  return st;
+}
+
+template <bool FMA>
+int fwt2d_reverse_strips(const FwtPlan& p, int S, const double* y, double* x, int rows, int cols,
+                         int lvlM, int lvlN, int batch, hipStream_t s) {
+  const long mat = (long)rows * cols, half = mat / 2;
+  double *T = nullptr, *B = nullptr;
+  JW_HIP_TRY(hipMallocAsync((void**)&T, sizeof(double) * mat * batch, s));
+  JW_HIP_TRY(hipMallocAsync((void**)&B, sizeof(double) * half * batch, s));
+  const Filters f = make_filters(p);
+  const int tail_lv = lvlM - S;
+  // level l (h = rows >> l) writes rows [0, h) of O_l: O_0 = T, then alternating with B
+  auto obuf = [&](int l) { return (l & 1) ? B : T; };
+  auto oms = [&](int l) { return (l & 1) ? half : mat; };
+  int st = JW_OK;
+  const double* a = y;  // approximations of the next (finer) level
+  long ms_a = mat;
+  if (tail_lv > 0) {
+    long h0 = p.tw;
+    for (int l = lvlM; l < log2_exact(rows); ++l) h0 <<= 1;  // FastWaveletTransform.java:137-141
+    if (!launch_tail<FMA>(p.M, p.kind, true, s, y, obuf(S), rows >> S, cols, mat, oms(S), (int)h0,
+                          p.tw, batch, f))
+      st = fail(JW_ERR_UNSUPPORTED, "no 2-D strip kernel for filter length %d", p.M);
+    a = obuf(S);
+    ms_a = oms(S);
+  }
+  for (int l = S - 1; l >= 0 && st == JW_OK; --l) {
+    const int h = rows >> l;
+    const Strip sp{a, y + (long)(h / 2) * cols, obuf(l), nullptr, ms_a, mat, oms(l), 0, cols, h};
+    if (!launch_strip<FMA>(p.M, p.kind, true, s, sp, batch, f)) st = fail(JW_ERR_UNSUPPORTED, "no 2-D strip kernel for filter length %d", p.M);
+    a = obuf(l);
+    ms_a = oms(l);
+  }
+  if (st == JW_OK) JW_HIP_TRY(hipGetLastError());
+  if (st == JW_OK) st = fwt_reverse_device(p, T, x, cols, lvlN, rows * batch, s);  // rows
+  (void)hipFreeAsync(B, s);
+  (void)hipFreeAsync(T, s);
+  return st;
+}
+
 // 2-D (BasicTransform.java:361-399): every row with lvlN, then every column with lvlM.
-// Fused path (power-of-two sides <= 4096, even M): rows with the LDS cascade, then the columns
-// in place with fwt_lines4 -- two passes over HBM.  Otherwise rows -> transpose -> rows ->
-// transpose.
+// Tall matrices (rows > 1024): rows with the LDS cascade, then the strip levels and the LDS
+// tail of the columns (fwt2d_forward_strips).  Otherwise, fused path (power-of-two sides <=
+// 4096, even M): rows with the LDS cascade, then the columns in place with fwt_lines4 -- two
+// passes over HBM.  Otherwise rows -> transpose -> rows -> transpose.
 int fwt2d_forward_device(const FwtPlan& p, const double* x, double* y, int rows, int cols,
                          int lvlM, int lvlN, int batch, hipStream_t s) {
+  if (const int S = strip_levels(p, rows, cols, lvlM); S > 0 && cols <= kLdsN) {
+    return p.arith == JW_ARITH_FMA
+               ? fwt2d_forward_strips<true>(p, S, x, y, rows, cols, lvlM, lvlN, batch, s)
+               : fwt2d_forward_strips<false>(p, S, x, y, rows, cols, lvlM, lvlN, batch, s);
+  }
   const bool fused = p.M % 2 == 0 && rows <= kLdsN && cols <= kLdsN && cols % kLines == 0 &&
                      rows >= 2 && !std::getenv("JW_FWT_GENERIC");
   if (fused) {
@@ -870,6 +1156,11 @@ int fwt2d_forward_device(const FwtPlan& p, const double* x, double* y, int rows,
 // 2-D reverse (BasicTransform.java:436-474): every column with lvlM, then every row with lvlN.
 int fwt2d_reverse_device(const FwtPlan& p, const double* y, double* x, int rows, int cols,
                          int lvlM, int lvlN, int batch, hipStream_t s) {
+  if (const int S = strip_levels(p, rows, cols, lvlM); S > 0) {
+    return p.arith == JW_ARITH_FMA
+               ? fwt2d_reverse_strips<true>(p, S, y, x, rows, cols, lvlM, lvlN, batch, s)
+               : fwt2d_reverse_strips<false>(p, S, y, x, rows, cols, lvlM, lvlN, batch, s);
+  }
   const bool fused = p.M % 2 == 0 && rows <= kLdsN && cols <= kLdsN && cols % kLines == 0 &&
                      rows >= 2 && !std::getenv("JW_FWT_GENERIC");
   if (fused) {

@@ -74,6 +74,30 @@ def test_fwt2d_bit_exact(wname, rows, cols, lvlM, lvlN):
     assert bits_equal(f.reverse(ref, lvlM, lvlN), orc.fwt2d_reverse(ref, lvlM, lvlN, wv))
 
 
+@pytest.mark.parametrize("wname", ["Haar1", "Haar1Orthogonal", "Daubechies8", "Symlet8",
+                                   "Daubechies2", "Coiflet5"])
+@pytest.mark.parametrize("rows,cols,lvlM,lvlN,tail", [
+    (256, 128, 8, 7, "64"),     # two strip levels, tail of 64 rows x 6 levels
+    (512, 64, 2, 6, "64"),      # every column level a strip: no tail
+    (128, 64, 7, 6, "64"),      # one strip level
+    (256, 64, 5, 6, "64"),      # tail with fewer levels than its length allows
+    (4096, 128, 12, 7, None),   # the cfg4 column geometry: 2 strips + 1024-row tail
+])
+def test_fwt2d_strip_columns_bit_exact(wname, rows, cols, lvlM, lvlN, tail, monkeypatch):
+    # tall matrices run the first column levels as row-strip kernels and the rest in an LDS
+    # tail (JW_FWT_TAIL shrinks the tail so small matrices take that path too)
+    if tail:
+        monkeypatch.setenv("JW_FWT_TAIL", tail)
+    wv = W.by_name(wname)
+    f = FastWaveletTransform(wv)
+    x = orc.fill_uniform(rows * cols, 17).reshape(rows, cols)
+    ref = orc.fwt2d_forward(x, lvlM, lvlN, wv)
+    assert bits_equal(f.forward(x, lvlM, lvlN), ref)
+    assert bits_equal(f.reverse(ref, lvlM, lvlN), orc.fwt2d_reverse(ref, lvlM, lvlN, wv))
+    fm = FastWaveletTransform(wv, arith="fma")
+    assert np.max(np.abs(fm.forward(x, lvlM, lvlN) - ref)) <= 1e-10 * np.max(np.abs(ref))
+
+
 def test_fwt2d_batch():
     wv = W.Daubechies8()
     f = FastWaveletTransform(wv)
