@@ -25,6 +25,14 @@ constexpr int kT = 8;                  // lines per workgroup (fast kernels)
 constexpr int kTile = 512 * (kT + 1);  // padded tile, also holds the 8 exchange buffers
 static_assert(kTile >= kT * fft::kXbuf, "tile must hold the exchange buffers");
 
+// Output staging slot of (output index n, line c): 8 lines per n, the line XOR-swizzled by
+// bits 3..5 of n.  A 16-byte element e sits on banks 4 (e mod 16) .. +3, so both sides are
+// bank-conflict free: the transposed write (8-lane groups: n = q + 8 k1 + 64 k2, k1 = lane & 7,
+// c fixed -> c ^ k1 distinct) and the coalescing read (16-lane groups: n = 8 w + (lane >> 3),
+// c = lane & 7 -> 8 (n & 1) + (c ^ w) distinct).  The padded [n][9] layout it replaces put 4
+// lanes of every write group on one bank group (SQ_LDS_BANK_CONFLICT = 62 % of LDS cycles).
+__device__ __forceinline__ int out_slot(int n, int c) { return 8 * n + (c ^ ((n >> 3) & 7)); }
+
 // IN_TILE: the line's inputs are strided (pass 1 over a natural-order array): stage 8 lines
 // through the tile.  TWID: apply the four-step twiddle W_N^(S n1 col) (pass 1).
 template <int S, bool IN_TILE, bool TWID, class In, class Out>
@@ -63,12 +71,12 @@ __device__ __forceinline__ void pass512_body(const In& in, const Out& out, long 
   }
   __syncthreads();
 #pragma unroll
-  for (int k2 = 0; k2 < 8; ++k2) tile[(q + 8 * k1 + 64 * k2) * (kT + 1) + c] = a[k2];
+  for (int k2 = 0; k2 < 8; ++k2) tile[out_slot(q + 8 * k1 + 64 * k2, c)] = a[k2];
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int n = (tid >> 3) + 64 * i, cc = tid & 7;
-    out(item, n, line0 + cc, tile[n * (kT + 1) + cc]);
+    out(item, n, line0 + cc, tile[out_slot(n, cc)]);
   }
 }
 
