@@ -164,7 +164,10 @@ struct ScaleIn {  // X[sig][k] * conj(psi_hat(omega_k, a_s)), k = N2 k1 + col; i
         e = w.p2 * om2;  // p2 = -0.5 sigma^2
         m *= om2;
       }
-      wv = make_double2(e < -746.0 ? 0.0 : m * exp(e), 0.0);
+      // Bins past the underflow point are exact zeros (as Math.exp gives): no exp, no X
+      // read.  A narrow band leaves whole 64-bin wave blocks zero, so the branch skips them.
+      if (e < -746.0) return make_double2(0.0, 0.0);
+      wv = make_double2(m * exp(e), 0.0);
     } else {
       double om = 2.0 * kPi * (double)k * fs / (double)N;  // createFrequencyAxis :453-456
       if (k > N / 2) om -= 2.0 * kPi * fs;

@@ -216,6 +216,38 @@ __device__ __forceinline__ d2 rev_pair_wrapped(const double* buf, int h, int u,
   return d2{acc[0], acc[1]};
 }
 
+// Taps of the reverse, in LDS, for the wrapped pairs' lane-dependent tap order:
+// tp[2t] = (sR[2t], sR[2t+1]), tp[2t+1] = (wR[2t], wR[2t+1]).  Filled by threads tid < M/2.
+template <int M>
+__device__ __forceinline__ void fill_rev_taps(d2* tp, int tid, const Filters& f) {
+  if (tid < M / 2) {
+    tp[2 * tid] = d2{f.sR[2 * tid], f.sR[2 * tid + 1]};
+    tp[2 * tid + 1] = d2{f.wR[2 * tid], f.wR[2 * tid + 1]};
+  }
+}
+
+// Wrapped pair (2u, 2u+1), u < M/2 - 1, h >= M: the same additions as rev_pair_wrapped in
+// the same order -- Java's scatter adds i ascending: the unwrapped taps t = u .. 0
+// (i = u - t), then the wrapped t = M/2-1 .. u+1 (i = u - t + h/2).  Step s of that order
+// is t = (u - s) mod M/2 with i = (u - t) mod h/2, so a uniform 8-step loop replaces the
+// predicated 2 x M/2 passes per output (taps from LDS: t is lane-dependent).
+template <bool FMA, int M, int KIND>
+__device__ __forceinline__ d2 rev_pair_rot(const double* buf, int h, int u, const d2* tp) {
+  constexpr int T2 = M / 2;
+  const int half = h >> 1;
+  double a0 = 0., a1 = 0.;
+#pragma unroll
+  for (int st = 0; st < T2; ++st) {
+    const int t = u - st >= 0 ? u - st : u - st + T2;
+    const int i = u - t >= 0 ? u - t : u - t + half;
+    const double av = buf[i], dv = buf[i + half];
+    const d2 sr = tp[2 * t], wr = tp[2 * t + 1];
+    a0 += contrib<FMA>(av, dv, sr.x, wr.x, KIND);
+    a1 += contrib<FMA>(av, dv, sr.y, wr.y, KIND);
+  }
+  return d2{a0, a1};
+}
+
 // The forward cascade on one line held in LDS (buf), by NTL threads (tid < NTL).  The
 // barriers are workgroup-wide: every line of the workgroup runs the same levels.
 template <bool FMA, int M, int NTL, int LEN = kLdsN>
@@ -272,7 +304,7 @@ __global__ __launch_bounds__(kNT2) void fwt_fwd_lds2(const double* __restrict__ 
 
 template <bool FMA, int M, int KIND, int NTL, int LEN = kLdsN>
 __device__ __forceinline__ void cascade_rev(double* buf, int n, int h0, int tw, int tid,
-                                            const Filters& f) {
+                                            const Filters& f, const d2* tp) {
   constexpr int P = (LEN / NTL / 2) < 1 ? 1 : LEN / NTL / 2;
   for (int h = h0; h <= n && h >= tw && h >= 2; h <<= 1) {
     const int half = h >> 1;
@@ -295,7 +327,9 @@ __device__ __forceinline__ void cascade_rev(double* buf, int n, int h0, int tw, 
       }
       if (u + NTL >= half) break;
     }
-    if (tid < nslow) o[0] = rev_pair_wrapped<FMA, M, KIND>(buf, h, tid, f);
+    if (tid < nslow)
+      o[0] = h >= M ? rev_pair_rot<FMA, M, KIND>(buf, h, tid, tp)
+                    : rev_pair_wrapped<FMA, M, KIND>(buf, h, tid, f);
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < P; ++r) {
@@ -311,12 +345,14 @@ __global__ __launch_bounds__(kNT2) void fwt_rev_lds2(const double* __restrict__ 
                                                     double* __restrict__ x, int n, int h0, int tw,
                                                     int kind, Filters f) {
   __shared__ __attribute__((aligned(16))) double buf[kLdsN];
+  __shared__ d2 tp[M];
   const int tid = threadIdx.x;
   const double* ys = y + (long)blockIdx.x * n;
   double* xs = x + (long)blockIdx.x * n;
   for (int i = 2 * tid; i < n; i += 2 * kNT2) *(d2*)&buf[i] = *(const d2*)&ys[i];
+  fill_rev_taps<M>(tp, tid, f);
   __syncthreads();
-  cascade_rev<FMA, M, KIND, kNT2>(buf, n, h0, tw, tid, f);
+  cascade_rev<FMA, M, KIND, kNT2>(buf, n, h0, tw, tid, f, tp);
   for (int i = 2 * tid; i < n; i += 2 * kNT2) *(d2*)&xs[i] = *(const d2*)&buf[i];
 }
 
@@ -378,11 +414,13 @@ __global__ __launch_bounds__(kNT2) void wpt_rev_lds(const double* __restrict__ y
                                                    double* __restrict__ x, int n, int h0, int tw,
                                                    Filters f) {
   __shared__ __attribute__((aligned(16))) double buf[kLdsN];
+  __shared__ d2 tp[M];
   constexpr int P = kLdsN / kNT2 / 2;
   const int tid = threadIdx.x;
   const double* ys = y + (long)blockIdx.x * n;
   double* xs = x + (long)blockIdx.x * n;
   for (int i = 2 * tid; i < n; i += 2 * kNT2) *(d2*)&buf[i] = *(const d2*)&ys[i];
+  fill_rev_taps<M>(tp, tid, f);
   __syncthreads();
   const int npairs = n >> 1;
   for (int h = h0; h <= n && h >= tw && h >= 2; h <<= 1) {
@@ -404,7 +442,8 @@ __global__ __launch_bounds__(kNT2) void wpt_rev_lds(const double* __restrict__ y
           }
           o[r] = d2{a0, a1};
         } else {
-          o[r] = rev_pair_wrapped<FMA, M, KIND>(buf + base, h, u, f);
+          o[r] = h >= M ? rev_pair_rot<FMA, M, KIND>(buf + base, h, u, tp)
+                        : rev_pair_wrapped<FMA, M, KIND>(buf + base, h, u, f);
         }
       }
     }
@@ -467,7 +506,9 @@ __global__ __launch_bounds__(NL * 256) void fwt_lines4(const double* in,
                                                            int nlines, int lvl_h0, int tw,
                                                            long tiles, Filters f) {
   __shared__ __attribute__((aligned(16))) double bufs[NL * kLinePad];
+  __shared__ d2 tp[M];
   const int tid = threadIdx.x, g = tid >> 8, lt = tid & 255;
+  if (REV) fill_rev_taps<M>(tp, tid, f);
   // XCD-aware tile order: workgroup b runs on XCD b % 8; give each XCD a contiguous range
   const long b = blockIdx.x;
   const long tile = (tiles % 8 == 0) ? (b % 8) * (tiles / 8) + b / 8 : b;
@@ -488,7 +529,7 @@ __global__ __launch_bounds__(NL * 256) void fwt_lines4(const double* in,
   }
   __syncthreads();
   if (REV) {
-    cascade_rev<FMA, M, KIND, 256>(buf, len, lvl_h0, tw, lt, f);
+    cascade_rev<FMA, M, KIND, 256>(buf, len, lvl_h0, tw, lt, f, tp);
   } else {
     cascade_fwd<FMA, M, 256>(buf, len, lvl_h0, tw, lt, f);
   }
@@ -570,7 +611,9 @@ __global__ __launch_bounds__(256) void fwt_strip_rev(Strip s, Filters f) {
   constexpr int T2 = M / 2;
   constexpr int NI = kST / 2 + T2 - 1;  // a/d rows of one strip
   __shared__ __attribute__((aligned(16))) double ta[NI * kSW], td[NI * kSW];
+  __shared__ d2 tp[M];
   const int tid = threadIdx.x, cp = tid & 31, rl = tid >> 5;
+  fill_rev_taps<M>(tp, tid, f);
   const int nchunk = s.cols / kSW;
   const int chunk = blockIdx.x % nchunk, strip = blockIdx.x / nchunk;
   const long mat = blockIdx.y;
@@ -585,24 +628,35 @@ __global__ __launch_bounds__(256) void fwt_strip_rev(Strip s, Filters f) {
   }
   __syncthreads();
   double* dst = s.dsta + mat * s.ms_dsta + c0 + 2 * cp;
+  // Strips past the first (k0/2 >= kST/2 >= T2 - 1) never wrap: compile-time taps t
+  // descending.  The first strip takes the rotated order (tstart = u there) with LDS taps.
+  const bool first = k0 / 2 < T2 - 1;
 #pragma unroll
   for (int q = 0; q < kST / 16; ++q) {
     const int ul = rl + 8 * q;  // local output pair: rows k0 + 2ul, k0 + 2ul + 1
     const int u = k0 / 2 + ul;
-    const int tstart = u >= T2 - 1 ? T2 - 1 : u;
     double e0 = 0., e1 = 0., o0 = 0., o1 = 0.;  // (even, odd row) x (column 0, column 1)
-#pragma unroll
-    for (int tt = 0; tt < T2; ++tt) {
-      int t = tstart - tt;
-      t = t < 0 ? t + T2 : t;
+    auto tap = [&](int t, double sr0, double wr0, double sr1, double wr1) {
       const int r = ul + (T2 - 1) - t;  // tile row of i = u - t
       const d2 av = *(const d2*)&ta[r * kSW + 2 * cp];
       const d2 dv = *(const d2*)&td[r * kSW + 2 * cp];
-      const double sr0 = f.sR[2 * t], wr0 = f.wR[2 * t], sr1 = f.sR[2 * t + 1], wr1 = f.wR[2 * t + 1];
       e0 += contrib<FMA>(av.x, dv.x, sr0, wr0, KIND);
       e1 += contrib<FMA>(av.y, dv.y, sr0, wr0, KIND);
       o0 += contrib<FMA>(av.x, dv.x, sr1, wr1, KIND);
       o1 += contrib<FMA>(av.y, dv.y, sr1, wr1, KIND);
+    };
+    if (!first) {
+#pragma unroll
+      for (int t = T2 - 1; t >= 0; --t) tap(t, f.sR[2 * t], f.wR[2 * t], f.sR[2 * t + 1], f.wR[2 * t + 1]);
+    } else {
+      const int tstart = u >= T2 - 1 ? T2 - 1 : u;
+#pragma unroll
+      for (int tt = 0; tt < T2; ++tt) {
+        int t = tstart - tt;
+        t = t < 0 ? t + T2 : t;
+        const d2 sr = tp[2 * t], wr = tp[2 * t + 1];
+        tap(t, sr.x, wr.x, sr.y, wr.y);
+      }
     }
     *(d2*)&dst[(long)(k0 + 2 * ul) * s.cols] = d2{e0, e1};
     *(d2*)&dst[(long)(k0 + 2 * ul + 1) * s.cols] = d2{o0, o1};
@@ -618,7 +672,9 @@ __global__ __launch_bounds__(1024) void fwt_cols_tail(const double* in, double* 
   constexpr int NTL = 1024 / kTailNL;
   constexpr int PAD = kTailLen + 2;  // 16-byte aligned lines; the transposed stores spread banks
   __shared__ __attribute__((aligned(16))) double bufs[kTailNL * PAD];
+  __shared__ d2 tp[M];
   const int tid = threadIdx.x, g = tid / NTL, lt = tid % NTL;
+  if (REV) fill_rev_taps<M>(tp, tid, f);
   const int nchunk = cols / kTailNL;
   const long mat = blockIdx.x / nchunk;
   const int line0 = (int)(blockIdx.x % nchunk) * kTailNL;
@@ -631,7 +687,7 @@ __global__ __launch_bounds__(1024) void fwt_cols_tail(const double* in, double* 
   __syncthreads();
   double* buf = bufs + g * PAD;
   if (REV) {
-    cascade_rev<FMA, M, KIND, NTL, kTailLen>(buf, len, lvl_h0, tw, lt, f);
+    cascade_rev<FMA, M, KIND, NTL, kTailLen>(buf, len, lvl_h0, tw, lt, f, tp);
   } else {
     cascade_fwd<FMA, M, NTL, kTailLen>(buf, len, lvl_h0, tw, lt, f);
   }
