@@ -47,6 +47,18 @@ __device__ __forceinline__ double contrib(double a, double d, double sr, double 
   return kind == JW_WAVELET_HAAR_ORTH ? .5 * c : c;
 }
 
+// acc + contrib: STRICT keeps Java's acc + ((a*sR) + (d*wR)); FMA folds both products into
+// the running sum, fma(d, wR, fma(a, sR, acc)) -- same taps, same order, 2 instead of 3
+// double ops per tap pair (the reverse cascades are VALU-heavy).
+template <bool FMA, int KIND>
+__device__ __forceinline__ double rev_acc(double acc, double a, double d, double sr, double wr) {
+  if constexpr (FMA && KIND != JW_WAVELET_HAAR_ORTH) {
+    return __builtin_fma(d, wr, __builtin_fma(a, sr, acc));
+  } else {
+    return acc + contrib<FMA>(a, d, sr, wr, KIND);
+  }
+}
+
 // Wavelet.forward output pair (i, i + h/2) from in[0..h).
 template <bool FMA>
 __device__ __forceinline__ void fwd_pair(const double* in, int h, int i, int M, const Filters& f,
@@ -242,8 +254,8 @@ __device__ __forceinline__ d2 rev_pair_rot(const double* buf, int h, int u, cons
     const int i = u - t >= 0 ? u - t : u - t + half;
     const double av = buf[i], dv = buf[i + half];
     const d2 sr = tp[2 * t], wr = tp[2 * t + 1];
-    a0 += contrib<FMA>(av, dv, sr.x, wr.x, KIND);
-    a1 += contrib<FMA>(av, dv, sr.y, wr.y, KIND);
+    a0 = rev_acc<FMA, KIND>(a0, av, dv, sr.x, wr.x);
+    a1 = rev_acc<FMA, KIND>(a1, av, dv, sr.y, wr.y);
   }
   return d2{a0, a1};
 }
@@ -304,7 +316,8 @@ __global__ __launch_bounds__(kNT2) void fwt_fwd_lds2(const double* __restrict__ 
 
 template <bool FMA, int M, int KIND, int NTL, int LEN = kLdsN>
 __device__ __forceinline__ void cascade_rev(double* buf, int n, int h0, int tw, int tid,
-                                            const Filters& f, const d2* tp) {
+                                            const Filters& f, const d2* tp,
+                                            double* gout = nullptr) {
   constexpr int P = (LEN / NTL / 2) < 1 ? 1 : LEN / NTL / 2;
   for (int h = h0; h <= n && h >= tw && h >= 2; h <<= 1) {
     const int half = h >> 1;
@@ -320,8 +333,8 @@ __device__ __forceinline__ void cascade_rev(double* buf, int n, int h0, int tw, 
 #pragma unroll
         for (int t = (M >> 1) - 1; t >= 0; --t) {
           const double av = buf[u - t], dv = buf[u - t + half];
-          a0 += contrib<FMA>(av, dv, f.sR[2 * t], f.wR[2 * t], KIND);  // KIND: compile-time
-          a1 += contrib<FMA>(av, dv, f.sR[2 * t + 1], f.wR[2 * t + 1], KIND);
+          a0 = rev_acc<FMA, KIND>(a0, av, dv, f.sR[2 * t], f.wR[2 * t]);  // KIND: compile-time
+          a1 = rev_acc<FMA, KIND>(a1, av, dv, f.sR[2 * t + 1], f.wR[2 * t + 1]);
         }
         o[r] = d2{a0, a1};
       }
@@ -330,6 +343,16 @@ __device__ __forceinline__ void cascade_rev(double* buf, int n, int h0, int tw, 
     if (tid < nslow)
       o[0] = h >= M ? rev_pair_rot<FMA, M, KIND>(buf, h, tid, tp)
                     : rev_pair_wrapped<FMA, M, KIND>(buf, h, tid, f);
+    if (gout && h == n) {
+      // last level straight to global memory (lane-consecutive 16-byte stores): no LDS
+      // round trip, no barriers; the caller skips its copy-out
+#pragma unroll
+      for (int r = 0; r < P; ++r) {
+        const int u = tid + r * NTL;
+        if (u < half) *(d2*)&gout[2 * u] = o[r];
+      }
+      return;
+    }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < P; ++r) {
@@ -352,8 +375,15 @@ __global__ __launch_bounds__(kNT2) void fwt_rev_lds2(const double* __restrict__ 
   for (int i = 2 * tid; i < n; i += 2 * kNT2) *(d2*)&buf[i] = *(const d2*)&ys[i];
   fill_rev_taps<M>(tp, tid, f);
   __syncthreads();
-  cascade_rev<FMA, M, KIND, kNT2>(buf, n, h0, tw, tid, f, tp);
-  for (int i = 2 * tid; i < n; i += 2 * kNT2) *(d2*)&xs[i] = *(const d2*)&buf[i];
+  // the last level (h = n) stores to xs itself when the cascade reaches it
+  const bool to_global = [&] {
+    int h = h0;
+    while (h < n && h >= tw && h >= 2) h <<= 1;
+    return h == n && h >= tw && h >= 2;
+  }();
+  cascade_rev<FMA, M, KIND, kNT2>(buf, n, h0, tw, tid, f, tp, to_global ? xs : nullptr);
+  if (!to_global)
+    for (int i = 2 * tid; i < n; i += 2 * kNT2) *(d2*)&xs[i] = *(const d2*)&buf[i];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -437,8 +467,8 @@ __global__ __launch_bounds__(kNT2) void wpt_rev_lds(const double* __restrict__ y
 #pragma unroll
           for (int t = (M >> 1) - 1; t >= 0; --t) {
             const double av = buf[base + u - t], dv = buf[base + u - t + half];
-            a0 += contrib<FMA>(av, dv, f.sR[2 * t], f.wR[2 * t], KIND);
-            a1 += contrib<FMA>(av, dv, f.sR[2 * t + 1], f.wR[2 * t + 1], KIND);
+            a0 = rev_acc<FMA, KIND>(a0, av, dv, f.sR[2 * t], f.wR[2 * t]);
+            a1 = rev_acc<FMA, KIND>(a1, av, dv, f.sR[2 * t + 1], f.wR[2 * t + 1]);
           }
           o[r] = d2{a0, a1};
         } else {
@@ -640,10 +670,10 @@ __global__ __launch_bounds__(256) void fwt_strip_rev(Strip s, Filters f) {
       const int r = ul + (T2 - 1) - t;  // tile row of i = u - t
       const d2 av = *(const d2*)&ta[r * kSW + 2 * cp];
       const d2 dv = *(const d2*)&td[r * kSW + 2 * cp];
-      e0 += contrib<FMA>(av.x, dv.x, sr0, wr0, KIND);
-      e1 += contrib<FMA>(av.y, dv.y, sr0, wr0, KIND);
-      o0 += contrib<FMA>(av.x, dv.x, sr1, wr1, KIND);
-      o1 += contrib<FMA>(av.y, dv.y, sr1, wr1, KIND);
+      e0 = rev_acc<FMA, KIND>(e0, av.x, dv.x, sr0, wr0);
+      e1 = rev_acc<FMA, KIND>(e1, av.y, dv.y, sr0, wr0);
+      o0 = rev_acc<FMA, KIND>(o0, av.x, dv.x, sr1, wr1);
+      o1 = rev_acc<FMA, KIND>(o1, av.y, dv.y, sr1, wr1);
     };
     if (!first) {
 #pragma unroll

@@ -28,13 +28,18 @@ def wavelet(name):
 def test_fwt_bit_exact_all_wavelets(wname):
     wv = wavelet(wname)
     f = FastWaveletTransform(wv)
+    fm = FastWaveletTransform(wv, arith="fma")
     for n, levels in [(2, [1]), (8, [0, 1, 3]), (64, [2, 6]), (1024, [10, 4])]:
         x = orc.fill_uniform(n, 3 + n)
         for lvl in levels:
             y = f.forward(x, lvl)
             ref = orc.fwt_forward(x, lvl, wv)
             assert bits_equal(y, ref), (n, lvl)
-            assert bits_equal(f.reverse(ref, lvl), orc.fwt_reverse(ref, lvl, wv)), (n, lvl)
+            rref = orc.fwt_reverse(ref, lvl, wv)
+            assert bits_equal(f.reverse(ref, lvl), rref), (n, lvl)
+            # FMA contract: same taps and order, fused products; north_star tolerance 1e-10
+            assert np.max(np.abs(fm.forward(x, lvl) - ref)) <= 1e-10 * np.max(np.abs(ref)), (n, lvl)
+            assert np.max(np.abs(fm.reverse(ref, lvl) - rref)) <= 1e-10 * np.max(np.abs(rref)), (n, lvl)
 
 
 @pytest.mark.parametrize("wname", ["Haar1", "Daubechies8", "Symlet8", "Haar1Orthogonal"])
@@ -96,6 +101,9 @@ def test_fwt2d_strip_columns_bit_exact(wname, rows, cols, lvlM, lvlN, tail, monk
     assert bits_equal(f.reverse(ref, lvlM, lvlN), orc.fwt2d_reverse(ref, lvlM, lvlN, wv))
     fm = FastWaveletTransform(wv, arith="fma")
     assert np.max(np.abs(fm.forward(x, lvlM, lvlN) - ref)) <= 1e-10 * np.max(np.abs(ref))
+    # FMA reverse (fused tap pairs): within the north_star's 1e-10 of the reference order
+    rref = orc.fwt2d_reverse(ref, lvlM, lvlN, wv)
+    assert np.max(np.abs(fm.reverse(ref, lvlM, lvlN) - rref)) <= 1e-10 * np.max(np.abs(rref))
 
 
 def test_fwt2d_batch():
