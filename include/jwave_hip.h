@@ -110,6 +110,16 @@ int jw_fwt2d_forward(const jw_fwt_plan* plan, const double* x, double* y, int ro
                      int lvlM, int lvlN, int batch, int where, void* stream);
 int jw_fwt2d_reverse(const jw_fwt_plan* plan, const double* y, double* x, int rows, int cols,
                      int lvlM, int lvlN, int batch, int where, void* stream);
+/* 3-D, space [d1][d2][d3] = Java's spc[i][j][k] (BasicTransform.java:509-565, :602-659):
+ * forward = the 2-D forward of every slab i with (lvlP, lvlQ) (rows of d3 samples with lvlQ,
+ * columns of d2 samples with lvlP), then the 1-D forward of every line along i with lvlR;
+ * reverse = the 2-D reverse of every slab, then the 1-D reverse along i (the reference's
+ * order).  BasicTransform.forward(double[][][]) passes lvlP = log2 d1, lvlQ = log2 d2,
+ * lvlR = log2 d3 (:487-495): callers that mirror it pass those. */
+int jw_fwt3d_forward(const jw_fwt_plan* plan, const double* x, double* y, int d1, int d2, int d3,
+                     int lvlP, int lvlQ, int lvlR, int batch, int where, void* stream);
+int jw_fwt3d_reverse(const jw_fwt_plan* plan, const double* y, double* x, int d1, int d2, int d3,
+                     int lvlP, int lvlQ, int lvlR, int batch, int where, void* stream);
 
 /* ======================================================================
  * CWT  (replaces ContinuousWaveletTransform.transformFFT :183-229 and

@@ -374,6 +374,43 @@ int jw_fwt2d_reverse(const jw_fwt_plan* plan, const double* y, double* x, int ro
   });
 }
 
+// 3-D: BasicTransform.forward/reverse(double[][][], lvlP, lvlQ, lvlR) (:509-659).  The
+// reference validates nothing itself; its first 1-D call fails first: forward -> slab 0's
+// rows (H, lvlQ), its columns (C, lvlP), then the lines along dimension 1 (R, lvlR);
+// reverse -> slab 0's columns (C, lvlP), rows (H, lvlQ), then (R, lvlR).
+int jw_fwt3d_forward(const jw_fwt_plan* plan, const double* x, double* y, int d1, int d2, int d3,
+                     int lvlP, int lvlQ, int lvlR, int batch, int where, void* stream) {
+  clear_error();
+  if (!plan) return fail(JW_ERR_ILLEGAL_ARGUMENT, "plan is null");
+  int st = fwt_check(d3, lvlQ, "forward");
+  if (st == JW_OK) st = fwt_check(d2, lvlP, "forward");
+  if (st == JW_OK) st = fwt_check(d1, lvlR, "forward");
+  if (st != JW_OK) return st;
+  if (st = check_where(where); st != JW_OK) return st;
+  if (batch <= 0) return batch == 0 ? JW_OK : fail(JW_ERR_ILLEGAL_ARGUMENT, "negative batch");
+  if (!x || !y) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
+  const size_t elems = (size_t)d1 * d2 * d3 * batch;
+  return run(where, stream, x, elems, y, elems, [&](const double* dx, double* dy, hipStream_t s) {
+    return fwt3d_forward_device(*plan, dx, dy, d1, d2, d3, lvlP, lvlQ, lvlR, batch, s);
+  });
+}
+int jw_fwt3d_reverse(const jw_fwt_plan* plan, const double* y, double* x, int d1, int d2, int d3,
+                     int lvlP, int lvlQ, int lvlR, int batch, int where, void* stream) {
+  clear_error();
+  if (!plan) return fail(JW_ERR_ILLEGAL_ARGUMENT, "plan is null");
+  int st = fwt_check(d2, lvlP, "reverse");
+  if (st == JW_OK) st = fwt_check(d3, lvlQ, "reverse");
+  if (st == JW_OK) st = fwt_check(d1, lvlR, "reverse");
+  if (st != JW_OK) return st;
+  if (st = check_where(where); st != JW_OK) return st;
+  if (batch <= 0) return batch == 0 ? JW_OK : fail(JW_ERR_ILLEGAL_ARGUMENT, "negative batch");
+  if (!x || !y) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
+  const size_t elems = (size_t)d1 * d2 * d3 * batch;
+  return run(where, stream, y, elems, x, elems, [&](const double* dy, double* dx, hipStream_t s) {
+    return fwt3d_reverse_device(*plan, dy, dx, d1, d2, d3, lvlP, lvlQ, lvlR, batch, s);
+  });
+}
+
 // ---------------------------------------------------------------- synthetic input
 // ---------------------------------------------------------------- CWT
 int jw_cwt_fft(int wavelet, const double* params, const double* x, long n, const double* scales,

@@ -1272,4 +1272,67 @@ int fwt2d_reverse_device(const FwtPlan& p, const double* y, double* x, int rows,
   return st;
 }
 
+// ---------------------------------------------------------------------------------------
+// 3-D (BasicTransform.java:509-565 forward, :602-659 reverse).  The space is [R][C][H]
+// (Java's spc[i][j][k]), batch-major.  Forward: every slab i gets the 2-D forward with
+// (lvlP, lvlQ) -- rows of H samples with lvlQ, then columns of C samples with lvlP -- and
+// then every (j, k) line along i (R samples, stride C*H) gets the 1-D forward with lvlR.
+// Reverse: the 2-D reverse per slab first, then the 1-D reverse along i (the reference's
+// order, not the mirror of the forward's).  The slabs are a batch of R*batch matrices for
+// the 2-D kernels; the lines along i are the columns of the [R][C*H] matrix.
+// ---------------------------------------------------------------------------------------
+namespace {
+// Columns of `batch` row-major [rows][cols] matrices: level lvl (forward) or the reverse of
+// level lvl, in -> out (in == out allowed).
+int fwt_columns(const FwtPlan& p, bool rev, const double* in, double* out, int rows, long cols,
+                int lvl, int batch, hipStream_t s) {
+  const size_t elems = (size_t)rows * cols * batch;
+  if (rows < 2 || lvl == 0) {  // forward(arr, 0) / reverse(arr, 0) copy the line
+    if (in != out) JW_HIP_TRY(hipMemcpyAsync(out, in, elems * sizeof(double), hipMemcpyDeviceToDevice, s));
+    return JW_OK;
+  }
+  if (p.M % 2 == 0 && rows <= kLdsN && cols % kLines == 0 && cols <= (1L << 30) &&
+      !std::getenv("JW_FWT_GENERIC")) {
+    int arg = lvl;
+    if (rev) {  // h0 = tw << (log2 rows - lvl), FastWaveletTransform.java:137-141
+      long h0 = p.tw;
+      for (int l = lvl; l < log2_exact(rows); ++l) h0 <<= 1;
+      arg = (int)h0;
+    }
+    const Filters f = make_filters(p);
+    const bool ok =
+        p.arith == JW_ARITH_FMA
+            ? launch_cols<true>(p.M, p.kind, rev, s, in, out, rows, (int)cols, arg, p.tw, batch, f)
+            : launch_cols<false>(p.M, p.kind, rev, s, in, out, rows, (int)cols, arg, p.tw, batch, f);
+    if (ok) {
+      JW_HIP_TRY(hipGetLastError());
+      return JW_OK;
+    }
+  }
+  double* t = nullptr;
+  JW_HIP_TRY(hipMallocAsync((void**)&t, sizeof(double) * elems, s));
+  int st = transpose(in, t, rows, (int)cols, batch, s);
+  if (st == JW_OK)
+    st = rev ? fwt_reverse_device(p, t, t, rows, lvl, (int)(cols * batch), s)
+             : fwt_forward_device(p, t, t, rows, lvl, (int)(cols * batch), s);
+  if (st == JW_OK) st = transpose(t, out, (int)cols, rows, batch, s);
+  JW_HIP_TRY(hipFreeAsync(t, s));
+  return st;
+}
+}  // namespace
+
+int fwt3d_forward_device(const FwtPlan& p, const double* x, double* y, int R, int C, int H,
+                         int lvlP, int lvlQ, int lvlR, int batch, hipStream_t s) {
+  int st = fwt2d_forward_device(p, x, y, C, H, lvlP, lvlQ, R * batch, s);
+  if (st != JW_OK) return st;
+  return fwt_columns(p, false, y, y, R, (long)C * H, lvlR, batch, s);
+}
+
+int fwt3d_reverse_device(const FwtPlan& p, const double* y, double* x, int R, int C, int H,
+                         int lvlP, int lvlQ, int lvlR, int batch, hipStream_t s) {
+  int st = fwt2d_reverse_device(p, y, x, C, H, lvlP, lvlQ, R * batch, s);
+  if (st != JW_OK) return st;
+  return fwt_columns(p, true, x, x, R, (long)C * H, lvlR, batch, s);
+}
+
 }  // namespace jw

@@ -75,6 +75,10 @@ int fwt2d_forward_device(const FwtPlan& p, const double* x, double* y, int rows,
                          int lvlM, int lvlN, int batch, hipStream_t s);
 int fwt2d_reverse_device(const FwtPlan& p, const double* y, double* x, int rows, int cols,
                          int lvlM, int lvlN, int batch, hipStream_t s);
+int fwt3d_forward_device(const FwtPlan& p, const double* x, double* y, int R, int C, int H,
+                         int lvlP, int lvlQ, int lvlR, int batch, hipStream_t s);
+int fwt3d_reverse_device(const FwtPlan& p, const double* y, double* x, int R, int C, int H,
+                         int lvlP, int lvlQ, int lvlR, int batch, hipStream_t s);
 int synth_uniform_device(double* x, long n, int batch, long seed0, hipStream_t s);
 
 // Device workspace that grows on demand (per calling thread, per device).

@@ -76,10 +76,14 @@ class FastWaveletTransform(WaveletTransform):
             _native._lib.jw_fwt_plan_destroy(plan)
 
     # ---- 1-D (WaveletTransform.forward/reverse(double[]) :77-112, FWT :71-153) ----
-    def forward(self, arr, level=None, lvlN=None):
+    def forward(self, arr, level=None, lvlN=None, lvlR=None):
+        if lvlR is not None:  # forward(double[][][], lvlP, lvlQ, lvlR)
+            return self._forward3d(arr, level, lvlN, lvlR)
         if lvlN is not None:  # forward(double[][], lvlM, lvlN)
             return self._forward2d(arr, level, lvlN)
         a = as_input(arr)
+        if len(a.shape) == 3:  # forward(double[][][]) (BasicTransform.java:487-495)
+            return self._forward3d(arr, *(_get_exponent(d) for d in a.shape))
         if len(a.shape) == 2:  # forward(double[][]) (BasicTransform.java:336-342)
             return self._forward2d(arr, _get_exponent(a.shape[0]), _get_exponent(a.shape[1]))
         if level is None:
@@ -92,10 +96,14 @@ class FastWaveletTransform(WaveletTransform):
             level = self.calcExponent(n)
         return self._run1d(a, level, batch=False, reverse=False)
 
-    def reverse(self, arr, level=None, lvlN=None):
+    def reverse(self, arr, level=None, lvlN=None, lvlR=None):
+        if lvlR is not None:
+            return self._reverse3d(arr, level, lvlN, lvlR)
         if lvlN is not None:
             return self._reverse2d(arr, level, lvlN)
         a = as_input(arr)
+        if len(a.shape) == 3:  # reverse(double[][][]) (BasicTransform.java:579-585)
+            return self._reverse3d(arr, *(_get_exponent(d) for d in a.shape))
         if len(a.shape) == 2:
             return self._reverse2d(arr, _get_exponent(a.shape[0]), _get_exponent(a.shape[1]))
         if level is None:
@@ -151,6 +159,33 @@ class FastWaveletTransform(WaveletTransform):
     def reverse2DBatch(self, images, lvlM, lvlN):
         return self._reverse2d(images, lvlM, lvlN, batch=True)
 
+    # ---- 3-D (BasicTransform.forward/reverse(double[][][], lvlP, lvlQ, lvlR) :509-659) ----
+    # Java applies lvlP to dimension 2, lvlQ to dimension 3 (the slab's 2-D transform) and
+    # lvlR to dimension 1; the no-level overloads pass the exponents of dimensions 1, 2, 3.
+    def _run3d(self, spc, lvlP, lvlQ, lvlR, batch, reverse):
+        a = as_input(spc)
+        L = _native.lib()
+        d1, d2, d3 = a.shape[-3], a.shape[-2], a.shape[-1]
+        B = a.shape[0] if batch else 1
+        out = a.empty(a.shape)
+        fn = L.jw_fwt3d_reverse if reverse else L.jw_fwt3d_forward
+        _native.check(fn(self._plan, a.ptr, out.ptr, d1, d2, d3, int(lvlP), int(lvlQ), int(lvlR),
+                         B, a.where, a.stream))
+        return out.result()
+
+    def _forward3d(self, spc, lvlP, lvlQ, lvlR, batch=False):
+        return self._run3d(spc, lvlP, lvlQ, lvlR, batch, False)
+
+    def _reverse3d(self, spc, lvlP, lvlQ, lvlR, batch=False):
+        return self._run3d(spc, lvlP, lvlQ, lvlR, batch, True)
+
+    def forward3DBatch(self, spaces, lvlP, lvlQ, lvlR):
+        """Batched extension: every space of ``spaces`` (B x d1 x d2 x d3)."""
+        return self._forward3d(spaces, lvlP, lvlQ, lvlR, batch=True)
+
+    def reverse3DBatch(self, spaces, lvlP, lvlQ, lvlR):
+        return self._reverse3d(spaces, lvlP, lvlQ, lvlR, batch=True)
+
     # ---- decompose / recompose (WaveletTransform.java:136-182) ----
     def decompose(self, arrTime):
         a = np.asarray(arrTime, dtype=np.float64)
@@ -201,3 +236,25 @@ class WaveletPacketTransform(FastWaveletTransform):
             return [self._reverse2d(m, lvlM, lvlN) for m in mat]
         x = self._t(self._rows(self._t(mat), lvlM, True))
         return self._rows(x, lvlN, True)
+
+    # 3-D (BasicTransform.java:509-659) over the packet transform: the 2-D packet transform of
+    # every slab, then the 1-D packet transform along dimension 1.
+    @staticmethod
+    def _stack(ms):
+        return __import__("torch").stack(ms) if hasattr(ms[0], "is_cuda") else np.stack(ms)
+
+    def _forward3d(self, spc, lvlP, lvlQ, lvlR, batch=False):
+        if batch:
+            return self._stack([self._forward3d(m, lvlP, lvlQ, lvlR) for m in spc])
+        y = self._stack([self._forward2d(m, lvlP, lvlQ) for m in spc])
+        d1 = y.shape[0]
+        lines = self._rows(self._t(y.reshape(d1, -1)), lvlR, False)
+        return self._t(lines).reshape(y.shape)
+
+    def _reverse3d(self, spc, lvlP, lvlQ, lvlR, batch=False):
+        if batch:
+            return self._stack([self._reverse3d(m, lvlP, lvlQ, lvlR) for m in spc])
+        x = self._stack([self._reverse2d(m, lvlP, lvlQ) for m in spc])
+        d1 = x.shape[0]
+        lines = self._rows(self._t(x.reshape(d1, -1)), lvlR, True)
+        return self._t(lines).reshape(x.shape)

@@ -499,6 +499,39 @@ void jwo_fwt2d_reverse(const double* y, int rows, int cols, int lvlM, int lvlN, 
   free(a); free(b);
 }
 
+/* 3-D: BasicTransform.forward(double[][][], lvlP, lvlQ, lvlR) :509-565 -- the 2-D forward
+ * of every slab i ([d2][d3]) with (lvlP, lvlQ), then the 1-D forward along i with lvlR;
+ * reverse :602-659 -- the 2-D reverse of every slab, then the 1-D reverse along i. */
+void jwo_fwt3d_forward(const double* x, int d1, int d2, int d3, int lvlP, int lvlQ, int lvlR,
+                       const double* sD, const double* wD, int M, int tw, double* y) {
+  const long slab = (long)d2 * d3;
+  double* a = (double*)malloc(sizeof(double) * d1);
+  double* b = (double*)malloc(sizeof(double) * d1);
+  for (int i = 0; i < d1; i++)
+    jwo_fwt2d_forward(x + i * slab, d2, d3, lvlP, lvlQ, sD, wD, M, tw, y + i * slab);
+  for (long jk = 0; jk < slab; jk++) {
+    for (int i = 0; i < d1; i++) a[i] = y[i * slab + jk];
+    jwo_fwt_forward(a, d1, lvlR, sD, wD, M, tw, b);
+    for (int i = 0; i < d1; i++) y[i * slab + jk] = b[i];
+  }
+  free(a); free(b);
+}
+
+void jwo_fwt3d_reverse(const double* y, int d1, int d2, int d3, int lvlP, int lvlQ, int lvlR,
+                       const double* sR, const double* wR, int M, int tw, int kind, double* x) {
+  const long slab = (long)d2 * d3;
+  double* a = (double*)malloc(sizeof(double) * d1);
+  double* b = (double*)malloc(sizeof(double) * d1);
+  for (int i = 0; i < d1; i++)
+    jwo_fwt2d_reverse(y + i * slab, d2, d3, lvlP, lvlQ, sR, wR, M, tw, kind, x + i * slab);
+  for (long jk = 0; jk < slab; jk++) {
+    for (int i = 0; i < d1; i++) a[i] = x[i * slab + jk];
+    jwo_fwt_reverse(a, d1, lvlR, sR, wR, M, tw, kind, b);
+    for (int i = 0; i < d1; i++) x[i * slab + jk] = b[i];
+  }
+  free(a); free(b);
+}
+
 /* ------------------------------------------------------------------------ */
 /* CWT FFT path: ContinuousWaveletTransform.transformFFT :183-229, padSignal :269-306, */
 /* createFrequencyAxis :450-459, ContinuousWavelet.fourierTransform :122-141,          */

@@ -86,6 +86,10 @@ void jwo_fwt2d_forward(const double* x, int rows, int cols, int lvlM, int lvlN, 
                        const double* wD, int M, int tw, double* y);
 void jwo_fwt2d_reverse(const double* y, int rows, int cols, int lvlM, int lvlN, const double* sR,
                        const double* wR, int M, int tw, int kind, double* x);
+void jwo_fwt3d_forward(const double* x, int d1, int d2, int d3, int lvlP, int lvlQ, int lvlR,
+                       const double* sD, const double* wD, int M, int tw, double* y);
+void jwo_fwt3d_reverse(const double* y, int d1, int d2, int d3, int lvlP, int lvlQ, int lvlR,
+                       const double* sR, const double* wR, int M, int tw, int kind, double* x);
 
 /* ---- CWT FFT path (transforms/ContinuousWaveletTransform.java:183-229) ---- */
 /* wavelet: 0 = Morlet(params[0]=fb, params[1]=fc), 1 = MexicanHat(params[0]=sigma),

@@ -156,6 +156,26 @@ def fwt2d_reverse(y, lvlM, lvlN, wavelet):
     return x
 
 
+def fwt3d_forward(x, lvlP, lvlQ, lvlR, wavelet):
+    """BasicTransform.forward(double[][][], lvlP, lvlQ, lvlR) (BasicTransform.java:509-565)."""
+    x = _f64(x)
+    y = np.empty_like(x)
+    sD, wD = _f64(wavelet.getScalingDeComposition()), _f64(wavelet.getWaveletDeComposition())
+    lib().jwo_fwt3d_forward(_p(x), *x.shape, lvlP, lvlQ, lvlR, _p(sD), _p(wD), sD.shape[0],
+                            wavelet.getTransformWavelength(), _p(y))
+    return y
+
+
+def fwt3d_reverse(y, lvlP, lvlQ, lvlR, wavelet):
+    """BasicTransform.reverse(double[][][], lvlP, lvlQ, lvlR) (BasicTransform.java:602-659)."""
+    y = _f64(y)
+    x = np.empty_like(y)
+    sR, wR = _f64(wavelet.getScalingReConstruction()), _f64(wavelet.getWaveletReConstruction())
+    lib().jwo_fwt3d_reverse(_p(y), *y.shape, lvlP, lvlQ, lvlR, _p(sR), _p(wR), sR.shape[0],
+                            wavelet.getTransformWavelength(), getattr(wavelet, "kind", 0), _p(x))
+    return x
+
+
 CWT_KINDS = {"morlet": 0, "mexhat": 1, "paul": 2, "dog": 3, "meyer": 4}
 
 

@@ -118,6 +118,31 @@ def test_fwt_validation():
         f.forward(np.ones(6))
 
 
+def test_fwt3d_validation_order():
+    # BasicTransform.forward(double[][][], lvlP, lvlQ, lvlR) (:509-565) fails at its first
+    # 1-D call: slab 0's rows (d3, lvlQ), then its columns (d2, lvlP), then dimension 1
+    # (d1, lvlR); the reverse (:602-659) checks slab 0's columns first.
+    f = FastWaveletTransform(W.Haar1())
+    x = np.zeros((4, 8, 16))
+    with pytest.raises(JWaveFailure, match="forward - given level is out of range"):
+        f.forward(x, 3, 5, 2)  # lvlQ = 5 > log2 16
+    with pytest.raises(JWaveFailure, match="forward - given level is out of range"):
+        f.forward(x, 4, 4, 2)  # lvlP = 4 > log2 8
+    with pytest.raises(JWaveFailure, match="forward - given level is out of range"):
+        f.forward(x, 3, 4, 3)  # lvlR = 3 > log2 4
+    with pytest.raises(JWaveFailure, match="given array length is not 2"):
+        f.forward(np.zeros((4, 8, 12)), 1, 1, 1)
+    with pytest.raises(JWaveFailure, match="reverse - given level is out of range"):
+        f.reverse(x, 4, 4, 2)
+    # the no-level overload passes log2 of dimensions 1, 2, 3 as (lvlP, lvlQ, lvlR)
+    # (:487-495): lvlQ = log2 8 = 3 for the 16-sample rows is fine, lvlP = log2 4 = 2 for
+    # the 8-sample columns too, but lvlR = log2 16 = 4 > log2 4 for dimension 1
+    with pytest.raises(JWaveFailure, match="forward - given level is out of range"):
+        f.forward(x)
+    t = Transform(f)
+    assert t.forward(x, 4, 4, 2) is None  # facade prints and returns null
+
+
 def test_precompute_filters_limits():
     m = MODWTTransform(W.Daubechies4())
     with pytest.raises(IllegalArgumentException, match="precomputeFilters - decomposition level must be at least 1"):

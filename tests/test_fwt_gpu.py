@@ -106,6 +106,57 @@ def test_fwt2d_strip_columns_bit_exact(wname, rows, cols, lvlM, lvlN, tail, monk
     assert np.max(np.abs(fm.reverse(ref, lvlM, lvlN) - rref)) <= 1e-10 * np.max(np.abs(rref))
 
 
+@pytest.mark.parametrize("wname,shape,lv", [
+    ("Haar1", (8, 16, 32), (4, 5, 3)),
+    ("Daubechies8", (16, 32, 64), (5, 6, 4)),
+    ("Daubechies4", (4, 64, 8), (6, 3, 2)),   # non-cubic, fused column path along dim 1
+    ("Symlet8", (32, 8, 4), (3, 2, 5)),
+    ("Coiflet1", (8, 8, 8), (2, 1, 3)),        # 6 taps, cubic
+    ("Haar1Orthogonal", (16, 16, 16), (4, 4, 4)),
+    ("Daubechies8", (2, 4, 8), (0, 2, 1)),
+])
+def test_fwt3d_bit_exact(wname, shape, lv):
+    # BasicTransform.forward/reverse(double[][][], lvlP, lvlQ, lvlR) (:509-659)
+    wv = W.by_name(wname)
+    f = FastWaveletTransform(wv)
+    x = orc.fill_uniform(int(np.prod(shape)), 23).reshape(shape)
+    ref = orc.fwt3d_forward(x, *lv, wv)
+    assert bits_equal(f.forward(x, *lv), ref)
+    rref = orc.fwt3d_reverse(ref, *lv, wv)
+    assert bits_equal(f.reverse(ref, *lv), rref)
+    fm = FastWaveletTransform(wv, arith="fma")
+    assert np.max(np.abs(fm.forward(x, *lv) - ref)) <= 1e-10 * np.max(np.abs(ref))
+    assert np.max(np.abs(fm.reverse(ref, *lv) - rref)) <= 1e-10 * np.max(np.abs(rref))
+
+
+def test_fwt3d_default_levels_and_batch():
+    wv = W.Daubechies8()
+    f = FastWaveletTransform(wv)
+    xs = np.stack([orc.fill_uniform(16 ** 3, 31 + b).reshape(16, 16, 16) for b in range(3)])
+    # forward(double[][][]) uses log2 of each dimension (:487-495)
+    assert bits_equal(f.forward(xs[0]), orc.fwt3d_forward(xs[0], 4, 4, 4, wv))
+    ys = f.forward3DBatch(xs, 3, 4, 2)
+    for b in range(3):
+        assert bits_equal(ys[b], orc.fwt3d_forward(xs[b], 3, 4, 2, wv))
+    xr = f.reverse3DBatch(ys, 3, 4, 2)
+    for b in range(3):
+        assert bits_equal(xr[b], orc.fwt3d_reverse(ys[b], 3, 4, 2, wv))
+
+
+def test_wpt3d_matches_composition():
+    from jwave.transforms.fwt import WaveletPacketTransform
+    wv = W.Daubechies4()
+    w = WaveletPacketTransform(wv)
+    x = orc.fill_uniform(8 * 16 * 32, 41).reshape(8, 16, 32)
+    y = w.forward(x, 3, 4, 2)
+    ref = np.stack([w.forward(x[i], 3, 4) for i in range(8)])
+    for j in range(16):
+        for k in range(32):
+            ref[:, j, k] = orc.wpt_forward(ref[:, j, k].copy(), 2, wv)
+    assert bits_equal(y, ref)
+    assert np.max(np.abs(w.reverse(y, 3, 4, 2) - x)) < 1e-10
+
+
 def test_fwt2d_batch():
     wv = W.Daubechies8()
     f = FastWaveletTransform(wv)

@@ -192,6 +192,25 @@ def test_haar_orthogonal_round_trip_exact_on_integers():
     assert bits_equal(orc.fwt_reverse(y, 5, wv), x)
 
 
+def test_fwt3d_is_slab_2d_then_dimension_1():
+    # BasicTransform.java:509-565 / :602-659 restated as compositions of the 2-D and 1-D
+    # oracles (slab transforms, then the lines along dimension 1), and the round trip
+    wv = W.Daubechies4()
+    x = orc.fill_uniform(8 * 16 * 32, 5).reshape(8, 16, 32)
+    y = orc.fwt3d_forward(x, 4, 5, 3, wv)
+    ref = np.stack([orc.fwt2d_forward(x[i], 4, 5, wv) for i in range(8)])
+    for j in range(16):
+        for k in range(32):
+            ref[:, j, k] = orc.fwt_forward(ref[:, j, k].copy(), 3, wv)
+    assert bits_equal(y, ref)
+    xr = np.stack([orc.fwt2d_reverse(y[i], 4, 5, wv) for i in range(8)])
+    for j in range(16):
+        for k in range(32):
+            xr[:, j, k] = orc.fwt_reverse(xr[:, j, k].copy(), 3, wv)
+    assert bits_equal(orc.fwt3d_reverse(y, 4, 5, 3, wv), xr)
+    assert np.max(np.abs(xr - x)) < 1e-10
+
+
 def test_fwt2d_round_trip():
     wv = W.Daubechies8()
     x = orc.fill_uniform(64 * 32, 11).reshape(64, 32)
