@@ -148,6 +148,15 @@ int jw_fwt3d_reverse(const jw_fwt_plan* plan, const double* y, double* x, int d1
 int jw_cwt_fft(int wavelet, const double* params, const double* x, long n, const double* scales,
                int ns, double sampling_rate, int padding, double* out_reim, int batch, int where,
                void* stream);
+/* ContinuousWaveletTransform.transform(signal, scales, fs) -- the direct time-domain CWT
+ * (:153-172, computeCoefficient :240-260; transformParallel :470-500 and
+ * transformParallelCustom :577-680 give the same values).  Same wavelet kinds and parameter
+ * blocks as jw_cwt_fft; out_reim is B x ns x n interleaved (re, im).  JW_ARITH_STRICT is
+ * bit-identical to the reference's sum order; JW_ARITH_FMA fuses each product into the sum.
+ * O(n x support x scale) work: the reference's path for short signals. */
+int jw_cwt_direct(int wavelet, const double* params, const double* x, long n,
+                  const double* scales, int ns, double sampling_rate, int arith, double* out_reim,
+                  int batch, int where, void* stream);
 
 /* ======================================================================
  * Synthetic input (bench / tests): java.util.Random(seed0 + b).nextDouble()*2-1 for

@@ -413,10 +413,8 @@ int jw_fwt3d_reverse(const jw_fwt_plan* plan, const double* y, double* x, int d1
 
 // ---------------------------------------------------------------- synthetic input
 // ---------------------------------------------------------------- CWT
-int jw_cwt_fft(int wavelet, const double* params, const double* x, long n, const double* scales,
-               int ns, double sampling_rate, int padding, double* out_reim, int batch, int where,
-               void* stream) {
-  clear_error();
+// The wavelet constructors' validation (kind and parameter block), shared by both CWT paths.
+static int cwt_wavelet_check(int wavelet, const double* params) {
   if (wavelet < JW_CWT_MORLET || wavelet > JW_CWT_MEYER)
     return fail(JW_ERR_ILLEGAL_ARGUMENT, "unknown continuous wavelet kind %d", wavelet);
   if (!params && wavelet != JW_CWT_MEYER)
@@ -444,6 +442,14 @@ int jw_cwt_fft(int wavelet, const double* params, const double* x, long n, const
     if (!(params[1] > 0))
       return fail(JW_ERR_ILLEGAL_ARGUMENT, "Width parameter sigma must be positive");
   }
+  return JW_OK;
+}
+
+int jw_cwt_fft(int wavelet, const double* params, const double* x, long n, const double* scales,
+               int ns, double sampling_rate, int padding, double* out_reim, int batch, int where,
+               void* stream) {
+  clear_error();
+  if (int st = cwt_wavelet_check(wavelet, params); st != JW_OK) return st;
   if (n < 0 || ns < 0 || batch < 0)
     return fail(JW_ERR_ILLEGAL_ARGUMENT, "negative size (n=%ld, ns=%d, batch=%d)", n, ns, batch);
   if (padding < JW_PAD_ZERO || padding > JW_PAD_CONSTANT)
@@ -460,6 +466,39 @@ int jw_cwt_fft(int wavelet, const double* params, const double* x, long n, const
              [&](const double* xi, double* o, hipStream_t s) {
                return cwt_fft_device(wavelet, params, xi, n, scales, ns, sampling_rate, padding,
                                      o, batch, s);
+             });
+}
+
+// ContinuousWaveletTransform.transform(signal, scales, fs) (:153-172) and its parallel
+// variants.  computeCoefficient (:240-260) evaluates wavelet(t, scale, 0) -- which throws
+// "Scale must be positive" for scale <= 0 (ContinuousWavelet.java:91-93) -- only inside a
+// non-empty window [max(0, t + lo), min(N - 1, t + hi)]: a negative scale turns the window
+// around (zeros, no exception), a zero scale throws.  Scales are checked in the reference's
+// loop order.
+int jw_cwt_direct(int wavelet, const double* params, const double* x, long n,
+                  const double* scales, int ns, double sampling_rate, int arith, double* out_reim,
+                  int batch, int where, void* stream) {
+  clear_error();
+  if (int st = cwt_wavelet_check(wavelet, params); st != JW_OK) return st;
+  if (n < 0 || ns < 0 || batch < 0)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "negative size (n=%ld, ns=%d, batch=%d)", n, ns, batch);
+  if (arith != JW_ARITH_STRICT && arith != JW_ARITH_FMA)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "unknown arithmetic mode %d", arith);
+  if (n > 0 && ns > 0 && !scales) return fail(JW_ERR_ILLEGAL_ARGUMENT, "scales are null");
+  for (int i = 0; i < ns && n > 0; ++i) {
+    double lo_f = 0, hi_f = 0;
+    cwt_direct_support(wavelet, params, scales[i], sampling_rate, &lo_f, &hi_f);
+    if (cwt_direct_window_nonempty(lo_f, hi_f, n) && scales[i] <= 0)
+      return fail(JW_ERR_ILLEGAL_ARGUMENT, "Scale must be positive");
+  }
+  int st = check_where(where);
+  if (st != JW_OK) return st;
+  if (n == 0 || ns == 0 || batch == 0) return JW_OK;
+  const size_t nin = (size_t)batch * n, nout = (size_t)batch * ns * n * 2;
+  return run(where, stream, x, nin, out_reim, nout,
+             [&](const double* xi, double* o, hipStream_t s) {
+               return cwt_direct_device(wavelet, params, xi, n, scales, ns, sampling_rate, arith,
+                                        o, batch, s);
              });
 }
 

@@ -63,6 +63,13 @@ int modwt_inverse_fft_device(const ModwtPlan& p, const double* coeffs, double* x
 int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
                    const double* scales_host, int ns, double fs, int padding, double* out,
                    int batch, hipStream_t s);
+int cwt_direct_device(int wavelet, const double* params, const double* x, long n,
+                      const double* scales, int ns, double fs, int arith, double* out, int batch,
+                      hipStream_t s);
+// Direct CWT window of one scale: (int)(support[0] a fs), (int)(support[1] a fs) as doubles.
+void cwt_direct_support(int wavelet, const double* params, double a, double fs, double* lo,
+                        double* hi);
+bool cwt_direct_window_nonempty(double lo, double hi, long n);
 int wpt_forward_device(const FwtPlan& p, const double* x, double* y, long n, int level, int batch,
                        hipStream_t s);
 int wpt_reverse_device(const FwtPlan& p, const double* y, double* x, long n, int level, int batch,

@@ -48,7 +48,7 @@ EXPORTS = (
     "jw_modwt_forward", "jw_modwt_inverse",
     "jw_fwt_plan_create", "jw_fwt_plan_destroy", "jw_fwt_forward", "jw_fwt_reverse",
     "jw_fwt2d_forward", "jw_fwt2d_reverse", "jw_fwt3d_forward", "jw_fwt3d_reverse",
-    "jw_synth_uniform", "jw_cwt_fft", "jw_wpt_forward", "jw_wpt_reverse",
+    "jw_synth_uniform", "jw_cwt_fft", "jw_cwt_direct", "jw_wpt_forward", "jw_wpt_reverse",
 )
 
 _lib = None
@@ -97,6 +97,7 @@ def lib():
     L.jw_fwt3d_reverse.argtypes = [c_dp, c_dp, c_dp, i, i, i, i, i, i, i, i, c_dp]
     L.jw_synth_uniform.argtypes = [c_dp, l, i, l, c_dp]
     L.jw_cwt_fft.argtypes = [i, c_dp, c_dp, l, c_dp, i, ctypes.c_double, i, c_dp, i, i, c_dp]
+    L.jw_cwt_direct.argtypes = [i, c_dp, c_dp, l, c_dp, i, ctypes.c_double, i, c_dp, i, i, c_dp]
     non_int = ("jw_last_error", "jw_version", "jw_modwt_plan_destroy", "jw_fwt_plan_destroy")
     for name in EXPORTS:
         if name not in non_int:

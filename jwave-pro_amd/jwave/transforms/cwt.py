@@ -154,6 +154,48 @@ class ContinuousWaveletTransform:
 
     transformFFTParallel = transformFFT  # same values (ContinuousWaveletTransform.java:511-565)
 
+    # ---- direct (time-domain) path: transform :141-172, computeCoefficient :240-260 ----
+    def _run_direct(self, x, scales, samplingRate, arith):
+        sc = np.ascontiguousarray(np.asarray(scales, dtype=np.float64).ravel())
+        B, n = x.shape
+        ns = sc.shape[0]
+        out = x.empty((B, ns, n, 2))
+        params = (ctypes.c_double * 2)(*self._wavelet.params())
+        _native.check(_native.lib().jw_cwt_direct(
+            self._wavelet._kind, params, x.ptr, n, sc.ctypes.data_as(ctypes.c_void_p), ns,
+            float(samplingRate), arith, out.ptr, B, x.where, x.stream))
+        return out
+
+    def transform(self, signal, scales, samplingRate=1.0, arith="strict"):
+        """Direct CWT on the GPU; arith "strict" is the reference's exact sum order."""
+        a = _native.JW_ARITH_FMA if arith == "fma" else _native.JW_ARITH_STRICT
+        x = as_input(np.asarray(signal, dtype=np.float64).reshape(1, -1))
+        out = self._run_direct(x, scales, samplingRate, a).obj
+        coeffs = out[0, ..., 0] + 1j * out[0, ..., 1]
+        n = coeffs.shape[1]
+        dt = 1.0 / samplingRate
+        time_axis = np.array([i * dt for i in range(n)])  # createTimeAxis :423-430
+        return CWTResult(coeffs, scales, time_axis, samplingRate, self._wavelet.getName())
+
+    def transformParallel(self, signal, scales, samplingRate=1.0):  # :470-500, same values
+        return self.transform(signal, scales, samplingRate)
+
+    def transformParallelCustom(self, signal, scales, samplingRate, parallelism):  # :577-680
+        return self.transform(signal, scales, samplingRate)
+
+    def transformBatch(self, signals, scales, samplingRate=1.0, arith="strict"):
+        """Direct CWT of B x n signals -> B x ns x n complex (numpy or device torch)."""
+        a = _native.JW_ARITH_FMA if arith == "fma" else _native.JW_ARITH_STRICT
+        x = as_input(signals)
+        if len(x.shape) == 1:
+            x = as_input(x.obj.reshape(1, -1))
+        out = self._run_direct(x, scales, samplingRate, a)
+        if out.device:
+            import torch
+            return torch.view_as_complex(out.obj)
+        o = out.obj
+        return o[..., 0] + 1j * o[..., 1]
+
     def transformFFTBatch(self, signals, scales, samplingRate=1.0):
         """B x n signals -> B x ns x n complex coefficients (numpy or device torch)."""
         x = as_input(signals)

@@ -1,3 +1,4 @@
+#define _GNU_SOURCE
 /*
  * jwave_oracle.c -- TEST INFRASTRUCTURE ONLY (see jwave_oracle.h).
  *
@@ -667,4 +668,126 @@ void jwo_modwt_fwdinv_batch(const double* x, long N, int J, const double* g, con
       jwo_modwt_inverse_direct(c, N, J, g, h, L, xr + (long)b * N);
     }
   }
+}
+
+/* ------------------------------------------------------------------------ */
+/* CWT direct path: ContinuousWaveletTransform.transform(signal, scales, fs) :153-172,      */
+/* computeCoefficient :240-260, ContinuousWavelet.wavelet(t, a, b) :90-102, and each       */
+/* class's wavelet(double t) and getEffectiveSupport().  Test infrastructure only.          */
+/* ------------------------------------------------------------------------ */
+static int jwo_java_d2i(double v) { /* Java (int) cast */
+  if (v != v) return 0;
+  if (v >= 2147483647.0) return 2147483647;
+  if (v <= -2147483648.0) return -2147483647 - 1;
+  return (int)v;
+}
+
+/* psi(t) of MorletWavelet.java:85-100, MexicanHatWavelet.java:85-95, PaulWavelet.java:142-150
+ * (+ complexPower :262-271), DOGWavelet.java:166-180 (+ Hermite :289-335, norm :357-366),
+ * MeyerWavelet.wavelet(double t) (+ sinc); support[] = getEffectiveSupport(). */
+void jwo_cwt_wavelet_t(int wavelet, const double* params, double t, double* re, double* im,
+                       double* support) {
+  const double PI = 3.14159265358979323846;
+  *re = 0.0; *im = 0.0;
+  if (wavelet == 0) { /* Morlet(fb, fc) */
+    double fb = params[0], fc = params[1];
+    double norm = 1.0 / sqrt(2.0 * PI * fb);
+    double envelope = exp(-t * t / (2.0 * fb));
+    double phase = 2.0 * PI * fc * t, sn, cs;
+    sincos(phase, &sn, &cs); /* one libm routine for both (the library does the same) */
+    *re = norm * envelope * cs;
+    *im = norm * envelope * sn;
+    support[0] = -(4.0 * sqrt(fb)); support[1] = 4.0 * sqrt(fb);
+  } else if (wavelet == 1) { /* Mexican hat(sigma) */
+    double sigma = params[0];
+    double nc = 2.0 / (sqrt(3.0 * sigma) * pow(PI, 0.25));
+    double tNorm = t / sigma, tNorm2 = tNorm * tNorm;
+    *re = nc * (1.0 - tNorm2) * exp(-0.5 * tNorm2);
+    support[0] = -5.0 * sigma; support[1] = 5.0 * sigma;
+  } else if (wavelet == 2) { /* Paul(m) */
+    int m = (int)params[0];
+    double fm = 1.0, f2m = 1.0;
+    for (int i = 2; i <= m; i++) fm *= i;
+    for (int i = 2; i <= 2 * m; i++) f2m *= i;
+    double nc = pow(2, m) * fm / sqrt(PI * f2m);
+    static const double ipr[4] = {1, 0, -1, 0}, ipi[4] = {0, 1, 0, -1};
+    double zr = 1.0, zi = -t; /* new Complex(1.0, -t) */
+    double mag = sqrt(zr * zr + zi * zi), arg = atan2(zi, zr);
+    double p = -(m + 1);
+    double newMag = pow(mag, p), newArg = p * arg;
+    double sn, cs;
+    sincos(newArg, &sn, &cs);
+    double pr = newMag * cs, pi = newMag * sn;
+    double ar = ipr[m % 4] * nc, ai = ipi[m % 4] * nc; /* _iPowerM.mul(_normConstant) */
+    *re = ar * pr - ai * pi;                             /* .mul(power) */
+    *im = ar * pi + ai * pr;
+    support[0] = -1.0; support[1] = 2.0 * (m + 1);
+  } else if (wavelet == 3) { /* DOG(n, sigma) */
+    int n = (int)params[0];
+    double sigma = params[1];
+    double c[12][12];
+    memset(c, 0, sizeof(c));
+    c[0][0] = 1.0;
+    if (n > 0) { c[1][0] = 0.0; c[1][1] = 2.0; }
+    for (int k = 2; k <= n; k++) {
+      for (int i = 1; i <= k; i++) if (i - 1 < k) c[k][i] += 2.0 * c[k - 1][i - 1];
+      for (int i = 0; i <= k - 2; i++) c[k][i] -= 2.0 * (k - 1) * c[k - 2][i];
+    }
+    double sign = ((n + 1) % 2 == 0) ? 1.0 : -1.0;
+    double df = 1.0;
+    for (int i = 2 * n - 1; i > 0; i -= 2) df *= i;
+    double nc = sqrt(df / (pow(2, n) * sqrt(PI) * pow(sigma, 2 * n + 1)));
+    double x = t / sigma;
+    double gaussian = exp(-0.5 * x * x);
+    double h = 0.0;
+    for (int i = n; i >= 0; i--) h = h * x + c[n][i] * sign;
+    *re = nc * h * gaussian;
+    double r = (3.0 + n / 2.0) * sigma;
+    support[0] = -r; support[1] = r;
+  } else { /* Meyer */
+    support[0] = -15.0; support[1] = 15.0;
+    if (fabs(t) > 15.0) return;
+    double envelope = exp(-0.5 * t * t / 25.0);
+    double om[3] = {0.7, 1.4 * 0.7, 0.5 * 0.7}, amp[3] = {1.0, 0.2, -0.1};
+    double value = 0.0;
+    for (int q = 0; q < 3; q++) {
+      double xx = om[q] * t, s;
+      if (fabs(xx) < 1e-10) { double x2 = xx * xx; s = 1.0 - x2 / 6.0 + x2 * x2 / 120.0; }
+      else s = sin(xx) / xx;
+      double term = q == 0 ? om[q] * s * envelope : amp[q] * om[q] * s * envelope;
+      value = q == 0 ? term : value + term;
+    }
+    value *= sqrt(2.0 / PI);
+    *re = value;
+  }
+}
+
+/* out[s][t] = (re, im) for one signal; returns 0, or -1 if a scale <= 0 meets a non-empty
+ * window (ContinuousWavelet.wavelet throws IllegalArgumentException there). */
+int jwo_cwt_direct(int wavelet, const double* params, const double* x, long n,
+                   const double* scales, int ns, double fs, double* out) {
+  double dt = 1.0 / fs;
+  for (int s = 0; s < ns; s++) {
+    double scale = scales[s], sup[2], wr, wi;
+    jwo_cwt_wavelet_t(wavelet, params, 0.0, &wr, &wi, sup);
+    for (long ti = 0; ti < n; ti++) {
+      long minIdx = ti + jwo_java_d2i(sup[0] * scale * fs);
+      long maxIdx = ti + jwo_java_d2i(sup[1] * scale * fs);
+      if (minIdx < 0) minIdx = 0;
+      if (maxIdx > n - 1) maxIdx = n - 1;
+      double sr = 0.0, si = 0.0;
+      for (long i = minIdx; i <= maxIdx; i++) {
+        if (scale <= 0) return -1;
+        double t = (double)(i - ti) * dt;
+        double vr, vi;
+        jwo_cwt_wavelet_t(wavelet, params, (t - 0.0) / scale, &vr, &vi, sup);
+        double nf = 1.0 / sqrt(scale);
+        vr = vr * nf; vi = -(vi * nf);           /* .mul(normFactor).conjugate() */
+        sr = sr + vr * x[i]; si = si + vi * x[i]; /* sum.add(waveletValue.mul(signal[i])) */
+      }
+      out[2 * ((long)s * n + ti)] = sr * dt;      /* sum.mul(dt) */
+      out[2 * ((long)s * n + ti) + 1] = si * dt;
+    }
+  }
+  return 0;
 }

@@ -101,6 +101,10 @@ void jwo_cwt_fft(int wavelet, const double* params, const double* x, long n,
 double jwo_cwt_wavelet_ft(int wavelet, const double* params, double omega, double scale);
 void jwo_cwt_wavelet_ft_c(int wavelet, const double* params, double omega, double scale,
                           double* re, double* im);
+void jwo_cwt_wavelet_t(int wavelet, const double* params, double t, double* re, double* im,
+                       double* support);
+int jwo_cwt_direct(int wavelet, const double* params, const double* x, long n,
+                   const double* scales, int ns, double fs, double* out);
 
 /* ---- batched wrappers for the CPU baseline (ForkJoin-equivalent, OpenMP over signals) ---- */
 void jwo_modwt_fwdinv_batch(const double* x, long N, int J, const double* g, const double* h,

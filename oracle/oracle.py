@@ -179,6 +179,22 @@ def fwt3d_reverse(y, lvlP, lvlQ, lvlR, wavelet):
 CWT_KINDS = {"morlet": 0, "mexhat": 1, "paul": 2, "dog": 3, "meyer": 4}
 
 
+def cwt_direct(x, kind, params, scales, fs=1.0):
+    """ContinuousWaveletTransform.transform (ContinuousWaveletTransform.java:153-172,
+    computeCoefficient :240-260): ns x n complex, one signal.  Raises ValueError where the
+    reference throws IllegalArgumentException("Scale must be positive")."""
+    x = _f64(x)
+    sc = _f64(scales)
+    prm = (ctypes.c_double * 2)(*(list(params) + [0.0, 0.0])[:2])
+    out = np.empty((sc.shape[0], x.shape[0], 2))
+    k = CWT_KINDS[kind] if isinstance(kind, str) else int(kind)
+    rc = lib().jwo_cwt_direct(k, prm, _p(x), ctypes.c_long(x.shape[0]), _p(sc), sc.shape[0],
+                              ctypes.c_double(fs), _p(out))
+    if rc != 0:
+        raise ValueError("Scale must be positive")
+    return out[..., 0] + 1j * out[..., 1]
+
+
 def cwt_wavelet_ft(wavelet, params, omega, scale):
     """ContinuousWavelet.fourierTransform(omega, scale, 0) as a complex number."""
     pr = _f64(list(params) + [0.0, 0.0])

@@ -240,6 +240,37 @@ def test_cwt_capi_paul_dog_meyer_validation():
                         0, None) == -1
 
 
+def test_cwt_direct_scale_validation():
+    # computeCoefficient (:240-260) calls wavelet(t, scale, 0) only inside a non-empty window:
+    # scale 0 -> "Scale must be positive" (ContinuousWavelet.java:91-93); a negative scale
+    # turns the window around and gives zeros without an exception (checked on the GPU)
+    from jwave.transforms.cwt import ContinuousWaveletTransform as CWT
+    from jwave.transforms.wavelets.continuous import MorletWavelet, PaulWavelet
+    for wv in (MorletWavelet(1.0, 1.0), PaulWavelet(4)):
+        with pytest.raises(IllegalArgumentException, match="Scale must be positive"):
+            CWT(wv).transform(np.ones(16), [2.0, 0.0])
+    with pytest.raises(ValueError, match="Scale must be positive"):
+        orc.cwt_direct(np.ones(16), "morlet", (1.0, 1.0), [2.0, 0.0])
+    assert np.all(orc.cwt_direct(np.ones(16), "morlet", (1.0, 1.0), [-2.0]) == 0)
+
+
+def test_cwt_direct_oracle_matches_host_closed_forms():
+    # the oracle's time-domain psi against the host mirror's closed forms (same formulas)
+    import ctypes
+    from jwave.transforms.wavelets.continuous import (MorletWavelet, MexicanHatWavelet,
+                                                      DOGWavelet)
+    for kind, wv in (("morlet", MorletWavelet(1.5, 0.8)), ("mexhat", MexicanHatWavelet(0.7)),
+                     ("dog", DOGWavelet(3, 1.2))):
+        prm = (ctypes.c_double * 2)(*wv.params())
+        for t in (-3.1, -0.4, 0.0, 0.25, 2.9):
+            re, im, sup = ctypes.c_double(), ctypes.c_double(), (ctypes.c_double * 2)()
+            orc.lib().jwo_cwt_wavelet_t(orc.CWT_KINDS[kind], prm, ctypes.c_double(t),
+                                        ctypes.byref(re), ctypes.byref(im), sup)
+            ref = complex(wv.wavelet(t))
+            assert abs(complex(re.value, im.value) - ref) <= 1e-14 * max(1.0, abs(ref))
+            assert list(sup) == list(wv.getEffectiveSupport())
+
+
 def test_cwt_result_accessors():
     from jwave.transforms import CWTResult
     c = np.array([[1 + 1j, -1 + 0j, 0j, -2 - 2j], [3 - 4j, 0 + 2j, -1 + 1e-300j, 1 - 1j]])
