@@ -39,6 +39,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1024, help="signals per GPU")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="modwt strong scaling (BASELINE configs[4]): this many signals in total, "
+                         "split over the ranks and processed in resident chunks of --chunk")
+    ap.add_argument("--chunk", type=int, default=1024, help="signals per launch (--global-batch)")
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--levels", type=int, default=8)
     ap.add_argument("--wavelet", default="Daubechies4")
@@ -275,17 +279,28 @@ def main():
     from jwave import MODWTTransform, _native
     from jwave.transforms import wavelets as W
 
-    B, n, J = args.batch, args.n, args.levels
+    n, J = args.n, args.levels
+    strong = args.global_batch > 0
+    if strong:  # configs[4]: a fixed total batch, sharded contiguously over the ranks
+        assert args.global_batch % world == 0, "--global-batch must divide over the ranks"
+        Bl = args.global_batch // world
+    else:       # weak scaling: every rank owns --batch signals
+        Bl = args.batch
+    B = min(Bl, args.chunk) if strong else Bl  # signals per launch
+    assert Bl % B == 0, "--chunk must divide the per-rank batch"
+    chunks = Bl // B
     wv = W.by_name(args.wavelet)
     lib = _native.lib()
     stream = torch.cuda.current_stream(dev)
     sptr = ctypes.c_void_p(stream.cuda_stream)
 
-    x = torch.empty((B, n), dtype=torch.float64, device=dev)
+    # inputs and reconstructions of the whole local batch stay resident; the coefficients
+    # of one launch's chunk are reused (sym8 J=6, 8192 signals on 1 GPU: 64 + 64 + 56 GB)
+    x = torch.empty((Bl, n), dtype=torch.float64, device=dev)
     c = torch.empty((B, J + 1, n), dtype=torch.float64, device=dev)
-    xr = torch.empty((B, n), dtype=torch.float64, device=dev)
-    seed0 = 42 + rank * B  # weak scaling: rank r owns global signals [r*B, (r+1)*B), seed 42 + g
-    _native.check(lib.jw_synth_uniform(ctypes.c_void_p(x.data_ptr()), n, B, seed0, sptr))
+    xr = torch.empty((Bl, n), dtype=torch.float64, device=dev)
+    seed0 = 42 + rank * Bl  # rank r owns global signals [r*Bl, (r+1)*Bl), seed 42 + g
+    _native.check(lib.jw_synth_uniform(ctypes.c_void_p(x.data_ptr()), n, Bl, seed0, sptr))
 
     def run(arith, steps, warmup):
         """Time `steps` fwd+inv steps; returns (elapsed_s max over ranks, fwd_ms, inv_ms)."""
@@ -293,31 +308,35 @@ def main():
         m.setConvolutionMethod(MODWTTransform.ConvolutionMethod.DIRECT)
         plan = m.initializeFilterCache()
 
-        def fwd():
-            _native.check(lib.jw_modwt_forward(plan, ctypes.c_void_p(x.data_ptr()),
+        def fwd(q):
+            _native.check(lib.jw_modwt_forward(plan, ctypes.c_void_p(x[q * B].data_ptr()),
                                                ctypes.c_void_p(c.data_ptr()), n, J, B,
                                                _native.JW_CONV_DIRECT, _native.JW_DEVICE, sptr))
 
-        def inv():
+        def inv(q):
             _native.check(lib.jw_modwt_inverse(plan, ctypes.c_void_p(c.data_ptr()),
-                                               ctypes.c_void_p(xr.data_ptr()), n, J, B,
+                                               ctypes.c_void_p(xr[q * B].data_ptr()), n, J, B,
                                                _native.JW_CONV_DIRECT, _native.JW_DEVICE, sptr))
 
         for _ in range(warmup):
-            fwd()
-            inv()
+            for q in range(chunks):
+                fwd(q)
+                inv(q)
         torch.cuda.synchronize()
-        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)]
+              for _ in range(steps * chunks)]
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for k in range(steps):
-            ev[k][0].record(stream)
-            fwd()
-            ev[k][1].record(stream)
-            inv()
-            ev[k][2].record(stream)
+            for q in range(chunks):  # one step = the whole local batch, chunk by chunk
+                e = ev[k * chunks + q]
+                e[0].record(stream)
+                fwd(q)
+                e[1].record(stream)
+                inv(q)
+                e[2].record(stream)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -325,8 +344,9 @@ def main():
         if world > 1:
             from jwave import distributed as jdist
             elapsed = jdist.max_over_ranks(elapsed, device=dev)
-        fwd_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / steps
-        inv_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / steps
+        # per launch (one chunk) averages
+        fwd_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
+        inv_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / len(ev)
         return elapsed, fwd_ms, inv_ms
 
     def spot_check(arith):
@@ -334,8 +354,9 @@ def main():
         import numpy as np
         import oracle as orc
         g, h = orc.modwt_filters(wv.getScalingDeComposition(), wv.getWaveletDeComposition())
-        sig = min(1, B - 1)
-        ref = orc.modwt_forward(orc.fill_uniform(n, seed0 + sig), J, g, h, "direct_nz")
+        sig = min(1, B - 1)  # of the last chunk, whose coefficients c still holds
+        ref = orc.modwt_forward(orc.fill_uniform(n, seed0 + (chunks - 1) * B + sig), J, g, h,
+                                "direct_nz")
         got = c[sig].cpu().numpy()
         if arith == "strict":
             return "bit-exact" if np.array_equal(got.view(np.uint64), ref.view(np.uint64)) else \
@@ -346,19 +367,27 @@ def main():
     alt = None
     if not args.no_alt:
         a_el, a_f, a_i = run(alt_arith, max(2, args.steps // 2), 1)
-        alt = {"arith": alt_arith, "value": round(B * n * world / (a_el / max(2, args.steps // 2)) / 1e6, 1),
+        alt = {"arith": alt_arith, "value": round(Bl * n * world / (a_el / max(2, args.steps // 2)) / 1e6, 1),
                "fwd_ms": round(a_f, 3), "inv_ms": round(a_i, 3)}
         if rank == 0 and not args.no_check:
             alt["spot_check_vs_oracle"] = spot_check(alt_arith)
 
     elapsed, fwd_ms, inv_ms = run(args.arith, args.steps, args.warmup)
     ms_per_step = elapsed * 1e3 / args.steps
-    total_samples = B * n * world
+    total_samples = Bl * n * world
     value = total_samples / (elapsed / args.steps) / 1e6
 
     # Reconstruction error over the whole local batch (max over ranks).
-    err = ((xr - x).abs().amax() / x.abs().amax()).item()
-    rms = torch.sqrt(torch.mean((xr - x) ** 2)).item()
+    # chunkwise: a whole-batch temporary would not fit beside the resident buffers
+    dmax = xmax = ssq = 0.0
+    for q in range(chunks):
+        d = xr[q * B:(q + 1) * B] - x[q * B:(q + 1) * B]
+        dmax = max(dmax, d.abs().amax().item())
+        xmax = max(xmax, x[q * B:(q + 1) * B].abs().amax().item())
+        ssq += torch.sum(d * d).item()
+        del d
+    err = dmax / xmax
+    rms = (ssq / (Bl * n)) ** 0.5
     if world > 1:
         from jwave import distributed as jdist
         err = jdist.max_over_ranks(err, device=dev)
@@ -391,15 +420,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (java.util.Random(42+signal).nextDouble()*2-1, generated in HBM)",
             "config": {
                 "workload": (f"MODWTTransform({args.wavelet}) forwardMODWT+inverseMODWT, J={J}, "
-                             f"N={n}, batch={B} per GPU, DIRECT convolution (BASELINE configs[1])"),
-                "wavelet": args.wavelet, "levels": J, "n": n, "batch_per_gpu": B,
-                "global_batch": B * world, "arith": args.arith,
+                             + (f"N={n}, {args.global_batch} signals over {world} GPU(s) in "
+                                f"chunks of {B}, DIRECT convolution (BASELINE configs[4])"
+                                if strong else
+                                f"N={n}, batch={B} per GPU, DIRECT convolution (BASELINE configs[1])")),
+                "wavelet": args.wavelet, "levels": J, "n": n, "batch_per_gpu": Bl,
+                "signals_per_launch": B, "global_batch": Bl * world, "arith": args.arith,
                 "parallelism": f"dp{world} (batch sharded, no data-path collective)",
             },
             "max_recon_error": err,

@@ -10,6 +10,7 @@ O="gpurun_out/bench_all_$TAG.jsonl"
 run() { timeout -k 10 600 python bench.py "$@" > gpurun_out/ba.log 2>&1 || { tail -5 gpurun_out/ba.log; exit 1; }; grep '^{' gpurun_out/ba.log >> "$O"; }
 run
 run --wavelet Symlet8 --levels 6 --no-cpu-baseline --no-alt
+run --wavelet Symlet8 --levels 6 --global-batch 8192 --steps 3 --warmup 1 --no-cpu-baseline --no-alt
 run --workload cwt --steps 3 --warmup 1
 run --workload fwt2d --steps 3 --warmup 1
 run --workload fwt2d --steps 3 --warmup 1 --arith strict --no-cpu-baseline
