@@ -247,10 +247,13 @@ template <bool FMA, int M, int KIND>
 __device__ __forceinline__ d2 rev_pair_rot(const double* buf, int h, int u, const d2* tp) {
   constexpr int T2 = M / 2;
   const int half = h >> 1;
+  // pairs past the wrap (u >= M/2 - 1) start at t = M/2 - 1: the plain descending order, so
+  // a whole wave can take this path (cascade_rev)
+  const int t0 = u < T2 - 1 ? u : T2 - 1;
   double a0 = 0., a1 = 0.;
 #pragma unroll
   for (int st = 0; st < T2; ++st) {
-    const int t = u - st >= 0 ? u - st : u - st + T2;
+    const int t = t0 - st >= 0 ? t0 - st : t0 - st + T2;
     const int i = u - t >= 0 ? u - t : u - t + half;
     const double av = buf[i], dv = buf[i + half];
     const d2 sr = tp[2 * t], wr = tp[2 * t + 1];
@@ -325,10 +328,16 @@ __device__ __forceinline__ void cascade_rev(double* buf, int n, int h0, int tw, 
     // are all thread tid = u of the first pass (nslow <= 32)
     const int nslow = h < M ? half : (M >> 1) - 1 < half ? (M >> 1) - 1 : half;
     d2 o[P];
+    // The wave holding the wrapped pairs (u < nslow, all in the first 64 threads' first
+    // pass) runs that pass in the rotated order for all its lanes -- one pass with LDS taps
+    // instead of the plain pass plus a second one for 7 lanes, which held every barrier.
+    const bool rot_wave = h >= M && NTL >= 64 && (tid >> 6) == 0;
 #pragma unroll
     for (int r = 0; r < P; ++r) {
       const int u = tid + r * NTL;
-      if (u < half && u >= nslow) {
+      if (r == 0 && rot_wave) {
+        if (u < half) o[0] = rev_pair_rot<FMA, M, KIND>(buf, h, u, tp);
+      } else if (u < half && u >= nslow) {
         double a0 = 0., a1 = 0.;
 #pragma unroll
         for (int t = (M >> 1) - 1; t >= 0; --t) {
@@ -340,7 +349,7 @@ __device__ __forceinline__ void cascade_rev(double* buf, int n, int h0, int tw, 
       }
       if (u + NTL >= half) break;
     }
-    if (tid < nslow)
+    if (tid < nslow && !rot_wave)
       o[0] = h >= M ? rev_pair_rot<FMA, M, KIND>(buf, h, tid, tp)
                     : rev_pair_wrapped<FMA, M, KIND>(buf, h, tid, f);
     if (gout && h == n) {
