@@ -31,6 +31,18 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "Msamples/s forward+inverse MODWT (db4, 8 levels, N=2^20); max recon error"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level table)
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "modwt_pmc_traffic.json")
+# cwt / fwt2d HBM bytes per step at their default configs (tools/pmc_traffic.sh,
+# tools/traffic_summary.py)
+TRAFFIC_STEP_FILE = os.path.join(ROOT, "profiles", "r01s4", "traffic_cwt_fwt2d.json")
+
+
+def step_traffic(workload, is_default):
+    if not is_default or not os.path.exists(TRAFFIC_STEP_FILE):
+        return None
+    try:
+        return json.load(open(TRAFFIC_STEP_FILE))[workload]["bytes_per_step"]
+    except Exception:
+        return None
 
 
 def parse():
@@ -167,8 +179,13 @@ def main_cwt(args, dev, rank, world):
             "parity": res,
             "roofline": {"bound": "hbm", "kernel": "jw_cwt_fft (all passes, one call)",
                          "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                         "algorithmic_bytes_per_launch": per_call},
+                         "frac": round(ach / HBM_PEAK_GBS, 4),
+                         "traffic": step_traffic("cwt", (B, n, ns) == (256, 1 << 18, 64)),
+                         "algorithmic_bytes_per_launch": per_call,
+                         "note": "one launch = one jw_cwt_fft call over the batch (all FFT "
+                                 "passes); traffic = rocprofv3 FETCH_SIZE*2 + WRITE_SIZE per call "
+                                 "(profiles/r01s4/traffic_cwt_fwt2d.json): the A workspace round "
+                                 "trip of the two-pass FFT is the excess over algorithmic"},
             "cpu_baseline": cpu}), flush=True)
 
 
@@ -255,7 +272,8 @@ def main_fwt2d(args, dev, rank, world):
             "max_recon_error": err, "spot_check_vs_oracle": check,
             "roofline": {"bound": "hbm", "kernel": "jw_fwt2d_forward + jw_fwt2d_reverse",
                          "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(ach / HBM_PEAK_GBS, 4),
+                         "traffic": step_traffic("fwt2d", B == 64),
                          "algorithmic_bytes_per_step": per, "fwd_ms": round(fms, 3),
                          "rev_ms": round(rms_, 3)},
             "cpu_baseline": None}), flush=True)
