@@ -594,7 +594,7 @@ __global__ __launch_bounds__(NL * 256) void fwt_lines4(const double* in,
 constexpr int kSW = 64;      // columns per strip workgroup (32 lanes x 2 columns)
 constexpr int kST = 32;      // output rows per strip workgroup
 constexpr int kTailNL = 16;  // columns per tail workgroup (128-byte row pieces)
-constexpr int kTailLen = 1024;
+constexpr int kTailLen = 256;
 
 struct Strip {  // one level's buffers, each [rows][cols] per matrix with its own matrix stride
   const double* src;  // forward: level input rows [0, h); reverse: approximations rows [0, h/2)
