@@ -9,9 +9,11 @@
 //   forward:  W_j = IFFT(X . H_j . prod_{i<j} G_i),   V_J = IFFT(X . prod_{i<=J} G_i)
 //   inverse:  S_J = FFT(V_J);  S_{j-1} = conj(G_j) S_j + conj(H_j) FFT(W_j);  x = IFFT(S_0)
 // (real parts taken at the end instead of per level: the same values up to rounding, inside
-// the FFT path's tolerance class).  Power-of-two N only (the four-step engine); other N are
-// served by the direct kernels, whose results are exact.
+// the FFT path's tolerance class).  Power-of-two N run the four-step engine directly; other N
+// (the reference's Bluestein lengths) run every length-N DFT as a chirp-z transform on it.
 #include <algorithm>
+#include <cmath>
+#include <vector>
 
 #include "jw_fft_passes.hpp"
 
@@ -118,12 +120,302 @@ long chunk_signals(long N, int J, int batch) {
   return std::max(1L, std::min<long>(batch, (1L << 30) / per_sig));
 }
 
+// ---------------------------------------------------------------------------------------
+// Other lengths (FastFourierTransform.java:259-324 takes them through Bluestein): the same
+// frequency-domain pyramid on natural-order spectra, each length-N DFT a chirp-z transform
+// over the power-of-two engine, M = 2^ceil(log2(2N - 1)):
+//   X_k = c_k^S * sum_n (x_n c_n^S) b_{k-n},  c_n = e^{i pi n^2 / N},  b_m = c_|m|^-S
+// (c^S: the conjugate for the forward transform, S = -1), the convolution as
+// IFFT_M(FFT_M(a) FFT_M(b)) / M.  Chirp angles are reduced exactly (n^2 mod 2N) on the host.
+// ---------------------------------------------------------------------------------------
+struct NatIn {  // complex rows of length M (natural order), element k = N2 k1 + col
+  static constexpr bool kStrided = true;
+  const cplx* a;
+  long M, N2;
+  __device__ cplx operator()(long item, long k1, long col) const {
+    return a[item * M + N2 * k1 + col];
+  }
+};
+struct NatOut1 {  // single pass: out[item][idx]
+  cplx* o;
+  long M;
+  __device__ void operator()(long item, long idx, long, cplx v) const { o[item * M + idx] = v; }
+};
+struct NatOut {  // four-step: out[item][n1 + N1 n2]
+  cplx* o;
+  long M, N1;
+  __device__ void operator()(long item, long idx, long line, cplx v) const {
+    o[item * M + line + N1 * idx] = v;
+  }
+};
+
+__device__ __forceinline__ cplx chirp(const cplx* w, long n, int S) {  // c_n^S
+  const cplx c = w[n];
+  return S < 0 ? make_double2(c.x, -c.y) : c;
+}
+
+// a[item][m] = m < N ? in[item][m] c_m^S : 0, m < M
+__global__ void bs_pre(const cplx* __restrict__ in, cplx* __restrict__ a, const cplx* w, long N,
+                       long M, long items, int S) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= items * M) return;
+  const long item = i / M, m = i - item * M;
+  a[i] = m < N ? fft::cmul(in[item * N + m], chirp(w, m, S)) : make_double2(0.0, 0.0);
+}
+__global__ void bs_mul(cplx* __restrict__ a, const cplx* __restrict__ bh, long M, long items) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= items * M) return;
+  a[i] = fft::cmul(a[i], bh[i % M]);
+}
+// out[item][k] = c_k^S conv[item][k] / M, k < N
+__global__ void bs_post(const cplx* __restrict__ conv, cplx* __restrict__ out, const cplx* w,
+                        long N, long M, long items, int S) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= items * N) return;
+  const long item = i / N, k = i - item * N;
+  const cplx v = fft::cmul(conv[item * M + k], chirp(w, k, S));
+  const double inv = 1.0 / (double)M;
+  out[i] = make_double2(v.x * inv, v.y * inv);
+}
+
+struct Bluestein {
+  long N = 0, M = 0;
+  Tables T;
+  cplx* w = nullptr;       // c_n, n < N
+  cplx* bh[2] = {};        // FFT_M(b) for S = -1 (index 0) and S = +1 (index 1)
+  cplx* ws = nullptr;      // 2 x items x M workspace
+  long ws_items = 0;
+};
+
+unsigned blocks(long n) { return (unsigned)((n + 255) / 256); }
+
+int fft_natural(int S, long M, long items, const cplx* in, cplx* out, cplx* A, hipStream_t s,
+                const Tables& T) {
+  const long N1 = fft::split_n1(M), N2 = M / N1;
+  return S < 0 ? fft::run_fft<-1>(M, items, NatIn{in, M, N2}, NatOut1{out, M}, NatOut{out, M, N1},
+                                  A, s, T, false)
+               : fft::run_fft<1>(M, items, NatIn{in, M, N2}, NatOut1{out, M}, NatOut{out, M, N1},
+                                 A, s, T, false);
+}
+
+int bluestein_init(Bluestein* B, long N, long max_items, hipStream_t s) {
+  B->N = N;
+  B->M = 1;
+  while (B->M < 2 * N - 1) B->M <<= 1;
+  const long M = B->M;
+  int st = fft::tables(M, &B->T);
+  if (st != JW_OK) return st;
+  std::vector<cplx> hw(N);
+  const long double pi = 3.141592653589793238462643383279502884L;
+  for (long n = 0; n < N; ++n) {
+    const long r = (long)(((__int128)n * n) % (2 * N));  // e^{i pi n^2/N} = e^{i pi r/N}
+    const long double ang = pi * (long double)r / (long double)N;
+    hw[n] = make_double2((double)cosl(ang), (double)sinl(ang));
+  }
+  B->ws_items = max_items;
+  JW_HIP_TRY(hipMallocAsync((void**)&B->w, N * sizeof(cplx), s));
+  JW_HIP_TRY(hipMallocAsync((void**)&B->bh[0], 2 * M * sizeof(cplx), s));
+  B->bh[1] = B->bh[0] + M;
+  JW_HIP_TRY(hipMallocAsync((void**)&B->ws, (size_t)2 * max_items * M * sizeof(cplx), s));
+  JW_HIP_TRY(hipMemcpyAsync(B->w, hw.data(), N * sizeof(cplx), hipMemcpyHostToDevice, s));
+  // b_m for both signs, then their FFTs (two items of length M)
+  std::vector<cplx> hb(2 * M, make_double2(0.0, 0.0));
+  for (int q = 0; q < 2; ++q) {  // q = 0: S = -1 -> b = c; q = 1: S = +1 -> b = conj(c)
+    for (long m = 0; m < N; ++m) {
+      const cplx c = q == 0 ? hw[m] : make_double2(hw[m].x, -hw[m].y);
+      hb[q * M + m] = c;
+      if (m > 0) hb[q * M + M - m] = c;
+    }
+  }
+  cplx* tmp = B->ws;  // the workspace's first 2M entries stage b
+  JW_HIP_TRY(hipMemcpyAsync(tmp, hb.data(), 2 * M * sizeof(cplx), hipMemcpyHostToDevice, s));
+  // pass workspace: the next 2M entries (ws holds 2 x max_items x M, max_items = batch (J+1) >= 2)
+  st = fft_natural(-1, M, 2, tmp, B->bh[0], B->ws + 2 * M, s, B->T);
+  if (st != JW_OK) return st;
+  JW_HIP_TRY(hipStreamSynchronize(s));  // hw / hb are host locals
+  return JW_OK;
+}
+
+void bluestein_free(Bluestein* B, hipStream_t s) {
+  (void)hipFreeAsync(B->ws, s);
+  (void)hipFreeAsync(B->bh[0], s);
+  (void)hipFreeAsync(B->w, s);
+}
+
+// items length-N DFTs (S = -1 forward, +1 reverse without 1/N), natural order in -> out
+int bluestein_dft(const Bluestein& B, int S, long items, const cplx* in, cplx* out, hipStream_t s) {
+  const long N = B.N, M = B.M;
+  for (long i0 = 0; i0 < items; i0 += B.ws_items) {
+    const long ni = std::min(B.ws_items, items - i0);
+    cplx *a = B.ws, *c = B.ws + ni * M;
+    hipLaunchKernelGGL(bs_pre, dim3(blocks(ni * M)), dim3(256), 0, s, in + i0 * N, a, B.w, N, M,
+                       ni, S);
+    int st = fft_natural(-1, M, ni, a, c, a, s, B.T);  // FFT_M(a) -> c (a is the pass workspace)
+    if (st != JW_OK) return st;
+    hipLaunchKernelGGL(bs_mul, dim3(blocks(ni * M)), dim3(256), 0, s, c, B.bh[S < 0 ? 0 : 1], M, ni);
+    st = fft_natural(1, M, ni, c, a, c, s, B.T);  // IFFT_M (no 1/M) -> a
+    if (st != JW_OK) return st;
+    hipLaunchKernelGGL(bs_post, dim3(blocks(ni * N)), dim3(256), 0, s, a, out + i0 * N, B.w, N, M,
+                       ni, S);
+    JW_HIP_TRY(hipGetLastError());
+  }
+  return JW_OK;
+}
+
+// R[0][f] = G(f), R[1][f] = H(f) for any N: e^{-2 pi i (f m mod N)/N}
+__global__ void filter_response_any(cplx* R, Taps taps, int L, long N) {
+  const long f = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= N) return;
+  cplx g = make_double2(0.0, 0.0), h = make_double2(0.0, 0.0);
+  for (int m = 0; m < L; ++m) {
+    double sn, cs;
+    sincospi(2.0 * (double)((f * m) % N) / (double)N, &sn, &cs);
+    g.x += taps.a[m] * cs;
+    g.y -= taps.a[m] * sn;
+    h.x += taps.b[m] * cs;
+    h.y -= taps.b[m] * sn;
+  }
+  R[f] = g;
+  R[N + f] = h;
+}
+
+__global__ void real_to_cplx(const double* __restrict__ x, cplx* __restrict__ y, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = make_double2(x[i], 0.0);
+}
+__global__ void cplx_re_scaled(const cplx* __restrict__ y, double* __restrict__ x, long n,
+                               double inv) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = y[i].x * inv;
+}
+// forward pyramid in frequency, natural order: Y[sig][r][k] = X[sig][k] F_r(k)
+__global__ void fwd_combine(const cplx* __restrict__ X, const cplx* __restrict__ R,
+                            cplx* __restrict__ Y, long N, int J, long nsig) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nsig * (J + 1) * N) return;
+  const long k = i % N, item = i / N, sig = item / (J + 1);
+  const int r = (int)(item - sig * (J + 1));
+  const int ng = r < J ? r : J - 1;
+  cplx f = make_double2(1.0, 0.0);
+  for (int q = 1; q <= ng; ++q) f = fft::cmul(f, R[(long)(((__int128)k << (q - 1)) % N)]);
+  f = fft::cmul(f, R[(r < J ? N : 0) + (long)(((__int128)k << ng) % N)]);
+  Y[i] = fft::cmul(X[sig * N + k], f);
+}
+// inverse: S[sig][k] from C[sig][r][k] = FFT(row r)
+__global__ void inv_combine(const cplx* __restrict__ C, const cplx* __restrict__ R,
+                            cplx* __restrict__ Sout, long N, int J, long nsig) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nsig * N) return;
+  const long sig = i / N, k = i - sig * N;
+  const cplx* c = C + sig * (long)(J + 1) * N;
+  cplx sv = c[(long)J * N + k];
+  for (int j = J; j >= 1; --j) {
+    const long f = (long)(((__int128)k << (j - 1)) % N);
+    const cplx g = R[f], h = R[N + f];
+    const cplx w = c[(long)(j - 1) * N + k];
+    sv = make_double2(g.x * sv.x + g.y * sv.y + h.x * w.x + h.y * w.y,
+                      g.x * sv.y - g.y * sv.x + h.x * w.y - h.y * w.x);
+  }
+  Sout[i] = sv;
+}
+
+int prepare_any(long N, const ModwtPlan& p, cplx** R, hipStream_t s) {
+  Taps taps;
+  for (int m = 0; m < p.L; ++m) {
+    taps.a[m] = p.g[m];
+    taps.b[m] = p.h[m];
+  }
+  JW_HIP_TRY(hipMallocAsync((void**)R, (size_t)2 * N * sizeof(cplx), s));
+  hipLaunchKernelGGL(filter_response_any, dim3(blocks(N)), dim3(256), 0, s, *R, taps, p.L, N);
+  JW_HIP_TRY(hipGetLastError());
+  return JW_OK;
+}
+
+// per-chunk signals for the general path: rows, spectra and the chirp workspace ~1 GB
+long chunk_any(long N, long M, int J, int batch) {
+  const long per_sig = ((long)(J + 1) * (2 * N + 2 * M) + 2 * N) * (long)sizeof(cplx);
+  return std::max(1L, std::min<long>(batch, (1L << 30) / per_sig));
+}
+
+int forward_any(const ModwtPlan& p, const double* x, double* coeffs, long N, int J, int batch,
+                hipStream_t s) {
+  cplx* R = nullptr;
+  int st = prepare_any(N, p, &R, s);
+  if (st != JW_OK) return st;
+  long M = 1;
+  while (M < 2 * N - 1) M <<= 1;
+  const long bc = chunk_any(N, M, J, batch);
+  Bluestein B;
+  st = bluestein_init(&B, N, bc * (J + 1), s);
+  cplx *X = nullptr, *Y = nullptr;
+  if (st == JW_OK) {
+    JW_HIP_TRY(hipMallocAsync((void**)&X, (size_t)bc * N * sizeof(cplx), s));
+    JW_HIP_TRY(hipMallocAsync((void**)&Y, (size_t)bc * (J + 1) * N * sizeof(cplx), s));
+  }
+  for (long b0 = 0; b0 < batch && st == JW_OK; b0 += bc) {
+    const long nb = std::min<long>(bc, batch - b0);
+    hipLaunchKernelGGL(real_to_cplx, dim3(blocks(nb * N)), dim3(256), 0, s, x + b0 * N, Y, nb * N);
+    st = bluestein_dft(B, -1, nb, Y, X, s);
+    if (st != JW_OK) break;
+    hipLaunchKernelGGL(fwd_combine, dim3(blocks(nb * (J + 1) * N)), dim3(256), 0, s, X, R, Y, N, J, nb);
+    st = bluestein_dft(B, 1, nb * (J + 1), Y, Y, s);
+    if (st != JW_OK) break;
+    hipLaunchKernelGGL(cplx_re_scaled, dim3(blocks(nb * (J + 1) * N)), dim3(256), 0, s, Y,
+                       coeffs + b0 * (long)(J + 1) * N, nb * (J + 1) * N, 1.0 / (double)N);
+    JW_HIP_TRY(hipGetLastError());
+  }
+  (void)hipFreeAsync(Y, s);
+  (void)hipFreeAsync(X, s);
+  bluestein_free(&B, s);
+  (void)hipFreeAsync(R, s);
+  return st;
+}
+
+int inverse_any(const ModwtPlan& p, const double* coeffs, double* x, long N, int J, int batch,
+                hipStream_t s) {
+  cplx* R = nullptr;
+  int st = prepare_any(N, p, &R, s);
+  if (st != JW_OK) return st;
+  long M = 1;
+  while (M < 2 * N - 1) M <<= 1;
+  const long bc = chunk_any(N, M, J, batch);
+  Bluestein B;
+  st = bluestein_init(&B, N, bc * (J + 1), s);
+  cplx *C = nullptr, *S = nullptr;
+  if (st == JW_OK) {
+    JW_HIP_TRY(hipMallocAsync((void**)&C, (size_t)bc * (J + 1) * N * sizeof(cplx), s));
+    JW_HIP_TRY(hipMallocAsync((void**)&S, (size_t)bc * N * sizeof(cplx), s));
+  }
+  for (long b0 = 0; b0 < batch && st == JW_OK; b0 += bc) {
+    const long nb = std::min<long>(bc, batch - b0);
+    hipLaunchKernelGGL(real_to_cplx, dim3(blocks(nb * (J + 1) * N)), dim3(256), 0, s,
+                       coeffs + b0 * (long)(J + 1) * N, C, nb * (J + 1) * N);
+    st = bluestein_dft(B, -1, nb * (J + 1), C, C, s);
+    if (st != JW_OK) break;
+    hipLaunchKernelGGL(inv_combine, dim3(blocks(nb * N)), dim3(256), 0, s, C, R, S, N, J, nb);
+    st = bluestein_dft(B, 1, nb, S, S, s);
+    if (st != JW_OK) break;
+    hipLaunchKernelGGL(cplx_re_scaled, dim3(blocks(nb * N)), dim3(256), 0, s, S, x + b0 * N,
+                       nb * N, 1.0 / (double)N);
+    JW_HIP_TRY(hipGetLastError());
+  }
+  (void)hipFreeAsync(S, s);
+  (void)hipFreeAsync(C, s);
+  bluestein_free(&B, s);
+  (void)hipFreeAsync(R, s);
+  return st;
+}
+
 }  // namespace
 
-bool modwt_fft_supported(long N) { return N >= 2 && (N & (N - 1)) == 0 && N <= (1L << 24); }
+static bool is_pow2(long N) { return (N & (N - 1)) == 0; }
+
+// power-of-two N: the four-step pyramid; other N (< 2^23): the chirp-z pyramid
+bool modwt_fft_supported(long N) { return N >= 2 && N <= (1L << 23); }
 
 int modwt_forward_fft_device(const ModwtPlan& p, const double* x, double* coeffs, long N, int J,
                              int batch, hipStream_t s) {
+  if (!is_pow2(N)) return forward_any(p, x, coeffs, N, J, batch, s);
   Tables T;
   cplx* R = nullptr;
   int st = prepare(N, p, &T, &R, s);
@@ -151,6 +443,7 @@ int modwt_forward_fft_device(const ModwtPlan& p, const double* x, double* coeffs
 
 int modwt_inverse_fft_device(const ModwtPlan& p, const double* coeffs, double* x, long N, int J,
                              int batch, hipStream_t s) {
+  if (!is_pow2(N)) return inverse_any(p, coeffs, x, N, J, batch, s);
   Tables T;
   cplx* R = nullptr;
   int st = prepare(N, p, &T, &R, s);
