@@ -69,9 +69,10 @@ int jw_modwt_plan_filters(const jw_modwt_plan* plan, double* g, double* h);
  * x: batch x n.  coeffs: batch x (levels+1) x n = [W_1..W_J, V_J] per signal.
  * Validation order and messages follow MODWTTransform.java:257-282; n == 0 is a no-op.
  * method: JW_CONV_* (the Java object's setConvolutionMethod state, passed per call).
- * JW_CONV_FFT with n a power of two runs the FFT-convolution path (MODWTTransform.java
- * :752-837: results within the FFT path's ~1e-12 of DIRECT); AUTO, DIRECT, and FFT at other
- * n run the direct kernels, which are bit-identical to the JVM's DIRECT path. */
+ * JW_CONV_FFT with 2 <= n <= 2^23 runs the FFT-convolution path (MODWTTransform.java
+ * :752-837: results within 1e-10 of DIRECT; non-power-of-two n through a chirp-z transform,
+ * as FastFourierTransform.java:259-324 does); AUTO, DIRECT, and FFT at other n run the
+ * direct kernels, which are bit-identical to the JVM's DIRECT path. */
 int jw_modwt_forward(const jw_modwt_plan* plan, const double* x, double* coeffs, long n,
                      int levels, int batch, int method, int where, void* stream);
 /* inverseMODWT(coefficients) (:337-375): coeffs batch x (levels+1) x n -> x batch x n. */
