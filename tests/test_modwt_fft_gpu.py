@@ -88,6 +88,36 @@ def test_fft_batch_and_reconstruction_cases():
             assert mse(xr[b], xs[b]) < 1e-10
 
 
+def test_fft_bluestein_batches_over_chunks():
+    # n = 70001, J = 3: the chirp-z pyramid holds ~24 signals per chunk (chunk_any), so 30
+    # signals take two chunks; every signal is checked per row against DIRECT
+    wv = W.Daubechies4()
+    g, h = ofilters(wv)
+    n, J, B = 70001, 3, 30
+    xs = np.stack([orc.fill_uniform(n, 100 + b) for b in range(B)])
+    m = MODWTTransform(wv)
+    m.setConvolutionMethod(ConvolutionMethod.FFT)
+    c = m.forwardMODWT(xs, J)
+    for b in (0, 23, 24, 29):
+        rows_close(c[b], orc.modwt_forward(xs[b], J, g, h, "direct_nz"))
+    xr = m.inverseMODWT(c)
+    assert np.max(np.abs(xr - xs)) < 1e-10
+
+
+@pytest.mark.parametrize("n,J", [(3, 1), (5, 2), (6, 2), (7, 2)])
+def test_fft_bluestein_tiny_lengths(n, J):
+    # filter longer than the signal (multi-wrap): the chirp-z path against DIRECT
+    wv = W.Daubechies4()
+    g, h = ofilters(wv)
+    x = orc.fill_uniform(n, 7 + n)
+    m = MODWTTransform(wv)
+    m.setConvolutionMethod(ConvolutionMethod.FFT)
+    c = m.forwardMODWT(x, J)
+    d = orc.modwt_forward(x, J, g, h, "direct_nz")
+    assert np.max(np.abs(c - d)) / np.max(np.abs(x)) < TOL
+    assert np.max(np.abs(m.inverseMODWT(c) - x)) < 1e-10
+
+
 def test_auto_runs_direct_bit_exact():
     wv = W.Daubechies4()
     g, h = ofilters(wv)
