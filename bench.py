@@ -57,6 +57,46 @@ def step_traffic(workload, is_default):
         return None
 
 
+def host_cpu():
+    """Threads the CPU baseline uses and what the host is: the GPU box allots 16 threads per
+    GPU (OMP_NUM_THREADS there); elsewhere every CPU this process may run on."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        affinity = os.cpu_count() or 1
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or affinity
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return threads, {"host_cpus": os.cpu_count(), "affinity_cpus": affinity, "cpu_model": model}
+
+
+def spawn_ranks(n):
+    """bench.py --gpus N without a launcher: start N rank processes of this script (one per
+    GPU, RANK = LOCAL_RANK = r, rendezvous on 127.0.0.1) and return the worst exit code.  This
+    parent makes no GPU call (it only waits), so nothing initialises HIP before the fork."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -78,13 +118,17 @@ def parse():
     ap.add_argument("--scales", type=int, default=64, help="cwt: number of log scales 2..1024")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="print each rank's identity and batch shard, then exit (no GPU work)")
     return ap.parse_args()
 
 
-def cpu_baseline(wname, n, J, threads):
-    """Oracle (C restatement of JWave's CPU path) on a bounded sample, OpenMP over signals."""
+def cpu_baseline(wname, n, J):
+    """Oracle (C restatement of JWave's CPU path) on a bounded sample, signals split by
+    ForkJoin-style recursive halving (ParallelTransform.java:222-335)."""
     import oracle as orc
     from jwave.transforms import wavelets as W
+    threads, host = host_cpu()
     wv = W.by_name(wname)
     g, h = orc.modwt_filters(wv.getScalingDeComposition(), wv.getWaveletDeComposition())
     # AUTO-faithful: at N=2^20 JWave's default performConvolution picks the FFT path for
@@ -100,17 +144,17 @@ def cpu_baseline(wname, n, J, threads):
     t0 = time.perf_counter()
     orc.modwt_fwdinv_batch(xs[:threads, :nd].copy(), J, g, h, use_fft=False, threads=threads)
     t_direct = time.perf_counter() - t0
-    return {
+    return dict({
         "value": ns * n / t_auto / 1e6,
         "unit": "Msamples/s",
         "cores": threads,
         "kind": "port",
         "sample": (f"{ns} signals x N={n} {wname} J={J} fwd+inv, AUTO path as JWave runs it "
-                   f"(FFT convolution, MODWTTransform.java:653), OpenMP over signals on {threads} threads: "
-                   f"{t_auto:.2f} s; DIRECT-faithful on {threads} x N={nd}: "
+                   f"(FFT convolution, MODWTTransform.java:653), ForkJoin halving over signals on "
+                   f"{threads} threads: {t_auto:.2f} s; DIRECT-faithful on {threads} x N={nd}: "
                    f"{threads * nd / t_direct / 1e6:.3f} Msamples/s"),
         "direct_value": threads * nd / t_direct / 1e6,
-    }
+    }, **host)
 
 
 def main_cwt(args, dev, rank, world):
@@ -171,13 +215,20 @@ def main_cwt(args, dev, rank, world):
                "vs_jwave_recurrence": float(np.max(np.abs(got - jw)) / np.max(np.abs(jw)))}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        xs = orc.fill_uniform(n, 7)
+        # transformFFTParallel (ContinuousWaveletTransform.java:511-565) per signal, signals in
+        # the outer ForkJoin pool, recurrence-twiddle FFT as the reference
+        threads, host = host_cpu()
+        nsig = threads
+        xs = np.stack([orc.fill_uniform(n, 7 + b) for b in range(nsig)])
         t0 = time.perf_counter()
-        orc.cwt_fft(xs, scales, 1.0, "morlet", (fb, fc), 1)
+        orc.cwt_fft_parallel_batch(xs, scales, 1.0, "morlet", (fb, fc), 1, threads=threads)
         tc = time.perf_counter() - t0
-        cpu = {"value": n / tc / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
-               "sample": f"1 signal x N={n}, {ns} scales, oracle transformFFT (recurrence-twiddle "
-                         f"radix-2 FFT like FastFourierTransform.java), 1 thread: {tc:.2f} s"}
+        cpu = dict({"value": nsig * n / tc / 1e6, "unit": "Msamples/s", "cores": threads,
+                    "kind": "port",
+                    "sample": f"{nsig} signals x N={n}, {ns} scales, oracle transformFFTParallel "
+                              f"(scales in parallel per signal, signals in the outer pool, "
+                              f"recurrence-twiddle radix-2 FFT like FastFourierTransform.java), "
+                              f"{threads} threads: {tc:.2f} s"}, **host)
     if rank == 0:
         ach = per_call / (ms * 1e-3) / 1e9
         print(json.dumps({
@@ -271,6 +322,21 @@ def main_fwt2d(args, dev, rank, world):
         check = "bit-exact" if np.array_equal(ref, got) else \
             f"normwise {np.max(np.abs(ref - got)) / np.max(np.abs(ref)):.3g}"
     lib.jw_fwt_plan_destroy(plan)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # ParallelTransform 2-D (ParallelTransform.java:70-126): per image, rows task then
+        # columns task forward, columns then rows reverse, leaves of <= 16 lines
+        threads, host = host_cpu()
+        nimg = 4
+        xs = np.stack([orc.fill_uniform(R * R, 11 + b).reshape(R, R) for b in range(nimg)])
+        t0 = time.perf_counter()
+        orc.fwt2d_fwdrev_parallel(xs, lvl, lvl, wv, threads=threads)
+        tc = time.perf_counter() - t0
+        cpu = dict({"value": nimg * R * R / tc / 1e6, "unit": "Mpixels/s", "cores": threads,
+                    "kind": "port",
+                    "sample": f"{nimg} images {R}x{R} Daubechies8 12x12 levels forward+reverse, "
+                              f"oracle ParallelTransform pattern (rows task -> columns task) on "
+                              f"{threads} threads: {tc:.2f} s"}, **host)
     if rank == 0:
         per = 64 * B * R * R  # 2 passes x (read + write) x 8 B, forward + reverse
         ach = per / ((fms + rms_) * 1e-3) / 1e9
@@ -289,19 +355,39 @@ def main_fwt2d(args, dev, rank, world):
                          "traffic": step_traffic("fwt2d", B == 64),
                          "algorithmic_bytes_per_step": per, "fwd_ms": round(fms, 3),
                          "rev_ms": round(rms_, 3)},
-            "cpu_baseline": None}), flush=True)
+            "cpu_baseline": cpu}), flush=True)
+
+
+def launch_check(args, rank, local_rank, world):
+    """--launch-check: each rank reports who it is and which signals it owns (no GPU)."""
+    from jwave import distributed as jdist
+    if world > 1:
+        jdist.init_from_env("gloo")
+    total = args.global_batch if args.global_batch > 0 else args.batch * world
+    start, count = jdist.shard_range(total, rank, world)
+    print(json.dumps({"rank": rank, "local_rank": local_rank, "world": world,
+                      "dist_world": dist.get_world_size() if world > 1 else 1,
+                      "global_batch": total, "shard_start": start, "shard_count": count,
+                      "seed_first": (42 if args.workload == "modwt" else 0) + start}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_check:
+        return launch_check(args, rank, local_rank, world)
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
         from jwave import distributed as jdist
         jdist.init_from_env("nccl", device=dev)
+        world = dist.get_world_size()  # the RCCL communicator's size (echoed as n_gpus)
     if args.workload == "cwt":
         return main_cwt(args, dev, rank, world)
     if args.workload == "fwt2d":
@@ -395,6 +481,69 @@ def main():
                 f"MISMATCH max {float(np.max(np.abs(got - ref)))}"
         return f"normwise {float(np.max(np.abs(got - ref)) / np.max(np.abs(ref))):.2e}"
 
+    def extra_paths(nb=16, reps=3):
+        """Two secondary figures on a 16-signal sub-batch (not the headline):
+        * JW_HOST: host double[] in, host double[] out -- what a JNI caller passing Java arrays
+          gets, PCIe staging included (pinned bounce buffers, cached HBM staging);
+        * AUTO: the reference's default ConvolutionMethod, which at this N takes the FFT path
+          (MODWTTransform.java:653); deviation of its coefficients from the oracle's restatement
+          of the reference's FFT path and from the exact DIRECT oracle (one signal)."""
+        import numpy as np
+        import oracle as orc
+        P = lambda a: ctypes.c_void_p(a.ctypes.data if isinstance(a, np.ndarray)  # noqa: E731
+                                      else a.data_ptr())
+        m = MODWTTransform(wv, arith=args.arith)  # AUTO, fftThreshold 4096
+        plan = m.initializeFilterCache()
+        xh = np.ascontiguousarray(x[:nb].cpu().numpy())
+        ch = np.empty((nb, J + 1, n))
+        xrh = np.empty((nb, n))
+
+        def host_step():
+            _native.check(lib.jw_modwt_forward(plan, P(xh), P(ch), n, J, nb, _native.JW_CONV_DIRECT,
+                                               _native.JW_HOST, None))
+            _native.check(lib.jw_modwt_inverse(plan, P(ch), P(xrh), n, J, nb, _native.JW_CONV_DIRECT,
+                                               _native.JW_HOST, None))
+
+        host_step()  # the staging buffers grow once
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            host_step()
+        th = (time.perf_counter() - t0) / reps
+        host = {"value": round(nb * n / th / 1e6, 1), "unit": "Msamples/s", "signals": nb,
+                "ms_per_call_pair": round(th * 1e3, 2),
+                "note": "jw_modwt_forward + jw_modwt_inverse with where=JW_HOST (host arrays "
+                        "in and out, DIRECT), PCIe staging included; never the headline value",
+                "recon_max_abs": float(np.max(np.abs(xrh - xh)))}
+        ca = torch.empty((nb, J + 1, n), dtype=torch.float64, device=dev)
+        xra = torch.empty((nb, n), dtype=torch.float64, device=dev)
+
+        def auto_step():
+            _native.check(lib.jw_modwt_forward(plan, P(x), P(ca), n, J, nb, _native.JW_CONV_AUTO,
+                                               _native.JW_DEVICE, sptr))
+            _native.check(lib.jw_modwt_inverse(plan, P(ca), P(xra), n, J, nb, _native.JW_CONV_AUTO,
+                                               _native.JW_DEVICE, sptr))
+
+        auto_step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            auto_step()
+        torch.cuda.synchronize()
+        ta = (time.perf_counter() - t0) / reps
+        g, h = orc.modwt_filters(wv.getScalingDeComposition(), wv.getWaveletDeComposition())
+        got = ca[0].cpu().numpy()
+        jw_fft = orc.modwt_forward(xh[0], J, g, h, "fft")
+        exact = orc.modwt_forward(xh[0], J, g, h, "direct_nz")
+        dev_rows = lambda a, b: max(float(np.max(np.abs(a[r] - b[r])) / np.max(np.abs(b[r])))  # noqa: E731
+                                    for r in range(J + 1))
+        auto = {"method": "AUTO -> FFT (N*M_j > 4096 at every level, MODWTTransform.java:653)",
+                "value": round(nb * n / ta / 1e6, 1), "unit": "Msamples/s", "signals": nb,
+                "max_row_normwise_vs_reference_fft_path": dev_rows(got, jw_fft),
+                "max_row_normwise_vs_exact_direct": dev_rows(got, exact),
+                "reference_fft_path_vs_exact_direct": dev_rows(jw_fft, exact),
+                "recon_max_abs": (xra - x[:nb]).abs().max().item()}
+        return host, auto
+
     alt_arith = "strict" if args.arith == "fma" else "fma"
     alt = None
     if not args.no_alt:
@@ -448,6 +597,7 @@ def main():
             "value": round(value, 1),
             "unit": "Msamples/s",
             "n_gpus": world,
+            "dist_world_size": dist.get_world_size() if world > 1 else 1,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
@@ -484,9 +634,10 @@ def main():
             "cpu_baseline": None,
             "other_arith": alt,
         }
+        if world == 1 and not args.no_check:
+            out["host_path"], out["auto_path"] = extra_paths()
         if world == 1 and not args.no_cpu_baseline:
-            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(args.wavelet, n, J, threads)
+            out["cpu_baseline"] = cpu_baseline(args.wavelet, n, J)
         print(json.dumps(out), flush=True)
 
     if world > 1:

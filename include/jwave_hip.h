@@ -80,6 +80,20 @@ int jw_modwt_inverse(const jw_modwt_plan* plan, const double* coeffs, double* x,
                      int levels, int batch, int method, int where, void* stream);
 
 /* ======================================================================
+ * FFT  (replaces FastFourierTransform.forward/reverse(Complex[]) :112-164)
+ * ====================================================================== */
+/* batch independent lines of n complex values, interleaved (re, im), batch-major.
+ * forward: X_k = sum_t x_t e^{-2 pi i t k / n};  reverse: x_t = (1/n) sum_k X_k e^{+2 pi i t k / n}
+ * (the reference's 1/n, :207-211).  n = 0: nothing; n = 1: a copy; powers of two run the
+ * four-step engine, other n <= 2^23 a chirp-z (Bluestein, :259-324) transform over it.
+ * Twiddles are correctly rounded (the reference builds them by recurrence, :188-201), so
+ * results agree with the reference's to its own rounding drift.  in == out is allowed. */
+int jw_fft_forward(const double* in_reim, double* out_reim, long n, int batch, int where,
+                   void* stream);
+int jw_fft_reverse(const double* in_reim, double* out_reim, long n, int batch, int where,
+                   void* stream);
+
+/* ======================================================================
  * FWT  (replaces FastWaveletTransform.forward/reverse(double[], level) :71/:119,
  *       the 1-D kernel Wavelet.forward/reverse :236/:277, and the 2-D
  *       BasicTransform.forward/reverse(double[][], lvlM, lvlN) :361/:436)

@@ -1,9 +1,13 @@
 // jw_capi.cpp -- the extern "C" boundary (include/jwave_hip.h): argument validation with the
 // reference's exception classes and messages, plan objects, host<->HBM staging.
+#include <algorithm>
 #include <cmath>
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <new>
+#include <vector>
 
 #include "jw_internal.hpp"
 
@@ -43,18 +47,108 @@ int floor_log2(long n) {
 
 bool is_binary(long n) { return n > 0 && (n & (n - 1)) == 0; }  // MathToolKit.isBinary :185-188
 
-// RAII staging of caller host buffers through HBM (JW_HOST).
-struct DevBuf {
-  double* p = nullptr;
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
+// JW_HOST staging (what a JNI crossing with double[] uses): per host thread and device, a
+// staging context whose HBM buffers only grow (no hipMalloc / hipFree per call: both
+// synchronise the device and would serialise concurrent Java threads), two pinned bounce
+// buffers that pipeline the pageable-memory copies (memcpy of chunk k+1 beside the DMA of
+// chunk k), and a private non-blocking stream when the caller passes none (threads never
+// meet on the null stream).
+constexpr size_t kPinDoubles = (size_t)4 << 20;  // 32 MiB per bounce buffer
+
+struct HostStage {
+  int dev = -1;
+  hipStream_t own = nullptr;
+  double* din = nullptr;
+  size_t din_cap = 0;
+  double* dout = nullptr;
+  size_t dout_cap = 0;
+  double* pin[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+
+  ~HostStage() {
+    if (dev < 0) return;
+    (void)hipSetDevice(dev);
+    if (own) (void)hipStreamSynchronize(own);
+    (void)hipFree(din);
+    (void)hipFree(dout);
+    for (int i = 0; i < 2; ++i) {
+      if (pin[i]) (void)hipHostFree(pin[i]);
+      if (ev[i]) (void)hipEventDestroy(ev[i]);
+    }
+    if (own) (void)hipStreamDestroy(own);
+  }
+
+  int init(int device) {
+    dev = device;
+    JW_HIP_TRY(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
+    for (int i = 0; i < 2; ++i) {
+      JW_HIP_TRY(hipHostMalloc((void**)&pin[i], kPinDoubles * sizeof(double),
+                               hipHostMallocDefault));
+      JW_HIP_TRY(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+    }
+    return JW_OK;
+  }
+
+  static int grow(double** p, size_t* cap, size_t n) {
+    if (n <= *cap) return JW_OK;
+    if (*p) JW_HIP_TRY(hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    JW_HIP_TRY(hipMalloc((void**)p, n * sizeof(double)));
+    *cap = n;
+    return JW_OK;
+  }
+
+  // host -> HBM through the bounce buffers; returns when the host buffer may be reused
+  int put(double* dst, const double* src, size_t n, hipStream_t s) {
+    for (size_t off = 0, k = 0; off < n; off += kPinDoubles, ++k) {
+      const size_t c = std::min(kPinDoubles, n - off);
+      const int b = (int)(k & 1);
+      JW_HIP_TRY(hipEventSynchronize(ev[b]));  // this buffer's previous DMA has landed
+      std::memcpy(pin[b], src + off, c * sizeof(double));
+      JW_HIP_TRY(hipMemcpyAsync(dst + off, pin[b], c * sizeof(double), hipMemcpyHostToDevice, s));
+      JW_HIP_TRY(hipEventRecord(ev[b], s));
+    }
+    return JW_OK;
+  }
+
+  // HBM -> host after the work queued on s; DMA of chunk k overlaps the memcpy of chunk k-1
+  int get(double* dst, const double* src, size_t n, hipStream_t s) {
+    size_t prev_off = 0, prev_c = 0;
+    int prev_b = -1;
+    for (size_t off = 0, k = 0; off < n; off += kPinDoubles, ++k) {
+      const size_t c = std::min(kPinDoubles, n - off);
+      const int b = (int)(k & 1);
+      JW_HIP_TRY(hipMemcpyAsync(pin[b], src + off, c * sizeof(double), hipMemcpyDeviceToHost, s));
+      JW_HIP_TRY(hipEventRecord(ev[b], s));
+      if (prev_b >= 0) {
+        JW_HIP_TRY(hipEventSynchronize(ev[prev_b]));
+        std::memcpy(dst + prev_off, pin[prev_b], prev_c * sizeof(double));
+      }
+      prev_off = off;
+      prev_c = c;
+      prev_b = b;
+    }
+    if (prev_b >= 0) {
+      JW_HIP_TRY(hipEventSynchronize(ev[prev_b]));
+      std::memcpy(dst + prev_off, pin[prev_b], prev_c * sizeof(double));
+    }
+    return JW_OK;
   }
 };
 
-int stage_in(DevBuf& d, const double* host, size_t n) {
-  if (n == 0) return JW_OK;
-  JW_HIP_TRY(hipMalloc((void**)&d.p, n * sizeof(double)));
-  if (host) JW_HIP_TRY(hipMemcpy(d.p, host, n * sizeof(double), hipMemcpyHostToDevice));
+int host_stage(HostStage** out) {
+  static thread_local std::vector<std::unique_ptr<HostStage>> stages;  // by device ordinal
+  int dev = 0;
+  JW_HIP_TRY(hipGetDevice(&dev));
+  if ((size_t)dev >= stages.size()) stages.resize(dev + 1);
+  if (!stages[dev]) {
+    auto st = std::make_unique<HostStage>();
+    const int rc = st->init(dev);
+    if (rc != JW_OK) return rc;
+    stages[dev] = std::move(st);
+  }
+  *out = stages[dev].get();
   return JW_OK;
 }
 
@@ -69,19 +163,38 @@ template <class F>
 int run(int where, void* stream, const double* in, size_t nin, double* out, size_t nout, F&& f) {
   hipStream_t s = (hipStream_t)stream;
   if (where == JW_DEVICE) return f(in, out, s);
-  DevBuf din, dout;
-  int st = stage_in(din, in, nin);
+  HostStage* hs = nullptr;
+  int st = host_stage(&hs);
   if (st != JW_OK) return st;
-  st = stage_in(dout, nullptr, nout);
-  if (st != JW_OK) return st;
-  st = f(din.p, dout.p, s);
-  if (st != JW_OK) return st;
+  if (!s) s = hs->own;
+  if ((st = HostStage::grow(&hs->din, &hs->din_cap, nin)) != JW_OK) return st;
+  if ((st = HostStage::grow(&hs->dout, &hs->dout_cap, nout)) != JW_OK) return st;
+  if ((st = hs->put(hs->din, in, nin, s)) != JW_OK) return st;
+  st = f(hs->din, hs->dout, s);
+  if (st != JW_OK) {
+    (void)hipStreamSynchronize(s);  // the staging buffers are reused by the next call
+    return st;
+  }
+  if ((st = hs->get(out, hs->dout, nout, s)) != JW_OK) return st;
   JW_HIP_TRY(hipStreamSynchronize(s));
-  if (nout) JW_HIP_TRY(hipMemcpy(out, dout.p, nout * sizeof(double), hipMemcpyDeviceToHost));
   return JW_OK;
 }
 
 }  // namespace
+
+hipError_t upload_async(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  void* tmp = std::malloc(bytes);
+  if (!tmp) return hipErrorOutOfMemory;
+  std::memcpy(tmp, src, bytes);
+  hipError_t e = hipMemcpyAsync(dst, tmp, bytes, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipLaunchHostFunc(s, [](void* p) { std::free(p); }, tmp);
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(s);
+    std::free(tmp);
+  }
+  return e;
+}
 }  // namespace jw
 
 using namespace jw;
@@ -151,9 +264,28 @@ static int modwt_method_check(int method) {
   return fail(JW_ERR_ILLEGAL_ARGUMENT, "unknown convolution method %d", method);
 }
 
-// FFT runs the spectral pyramid (jw_modwt_fft.hip) for power-of-two n; AUTO and DIRECT, and
-// FFT at other n, run the direct kernels (exact; within the FFT path's tolerance of it).
-static bool use_fft(int method, long n) { return method == JW_CONV_FFT && modwt_fft_supported(n); }
+// MODWTTransform.performConvolution AUTO (:640-664): a level's convolution takes the FFT path
+// when signal.length * filter.length > fftConvolutionThreshold, a Java int multiply (it wraps
+// for N*M >= 2^31, :653).  The up-sampled level-j filter has M_j = (L-1)*2^(j-1) + 1 taps.
+static bool auto_level_fft(long n, int L, int j, int threshold) {
+  const uint32_t m = (uint32_t)(L - 1) * (1u << (j - 1)) + 1u;
+  const int32_t prod = (int32_t)((uint32_t)n * m);
+  return prod > threshold;
+}
+
+// FFT runs the frequency-domain pyramid (jw_modwt_fft.hip).  AUTO runs it when the reference's
+// rule sends any level's convolution to its FFT path (the pyramid is evaluated as a whole in
+// the frequency domain, so a plan mixing DIRECT and FFT levels runs entirely as FFT: the DIRECT
+// levels' values agree to rounding) and the exact direct kernels otherwise.  Lengths outside
+// the FFT engine's range run DIRECT.
+static bool use_fft(const ModwtPlan& p, int method, long n, int levels) {
+  if (!modwt_fft_supported(n)) return false;
+  if (method == JW_CONV_FFT) return true;
+  if (method != JW_CONV_AUTO) return false;
+  for (int j = 1; j <= levels; ++j)
+    if (auto_level_fft(n, p.L, j, p.fft_threshold)) return true;
+  return false;
+}
 
 int jw_modwt_forward(const jw_modwt_plan* plan, const double* x, double* coeffs, long n,
                      int levels, int batch, int method, int where, void* stream) {
@@ -185,7 +317,7 @@ int jw_modwt_forward(const jw_modwt_plan* plan, const double* x, double* coeffs,
   const size_t nin = (size_t)n * batch, nout = (size_t)n * batch * (levels + 1);
   return run(where, stream, x, nin, coeffs, nout,
              [&](const double* dx, double* dc, hipStream_t s) {
-               return use_fft(method, n)
+               return use_fft(*plan, method, n, levels)
                           ? modwt_forward_fft_device(*plan, dx, dc, n, levels, batch, s)
                           : modwt_forward_device(*plan, dx, dc, n, levels, batch, s);
              });
@@ -211,10 +343,38 @@ int jw_modwt_inverse(const jw_modwt_plan* plan, const double* coeffs, double* x,
   const size_t nin = (size_t)n * batch * (levels + 1), nout = (size_t)n * batch;
   return run(where, stream, coeffs, nin, x, nout,
              [&](const double* dc, double* dx, hipStream_t s) {
-               return use_fft(method, n)
+               return use_fft(*plan, method, n, levels)
                           ? modwt_inverse_fft_device(*plan, dc, dx, n, levels, batch, s)
                           : modwt_inverse_device(*plan, dc, dx, n, levels, batch, s);
              });
+}
+
+// ---------------------------------------------------------------- FFT
+// FastFourierTransform.forward / reverse(Complex[]) (FastFourierTransform.java:112-164):
+// length 0 -> nothing, 1 -> a copy, powers of two -> Cooley-Tukey, others -> Bluestein.
+static int fft_call(int S, const double* in, double* out, long n, int batch, int where,
+                    void* stream) {
+  clear_error();
+  if (n < 0 || batch < 0)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "negative length %ld or batch %d", n, batch);
+  int st = check_where(where);
+  if (st != JW_OK) return st;
+  if (n == 0 || batch == 0) return JW_OK;
+  if (!in || !out) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
+  const size_t elems = (size_t)2 * n * batch;
+  return run(where, stream, in, elems, out, elems, [&](const double* di, double* dout, hipStream_t s) {
+    return fft_device(S, di, dout, n, batch, s);
+  });
+}
+
+int jw_fft_forward(const double* in_reim, double* out_reim, long n, int batch, int where,
+                   void* stream) {
+  return fft_call(-1, in_reim, out_reim, n, batch, where, stream);
+}
+
+int jw_fft_reverse(const double* in_reim, double* out_reim, long n, int batch, int where,
+                   void* stream) {
+  return fft_call(1, in_reim, out_reim, n, batch, where, stream);
 }
 
 // ---------------------------------------------------------------- FWT

@@ -252,11 +252,12 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   // (run_fft512_pipelined); env JW_CWT_PIPE=0 runs the groups one after the other (A/B runs).
   const char* gpp = std::getenv("JW_CWT_PIPE");
   const bool pipe = N == (1L << 18) && (long)batch * ns > gpair && !(gpp && gpp[0] == '0');
+  StreamAllocs mem(s);
   cplx *X = nullptr, *A = nullptr;
   double* dsc = nullptr;
   const long a_items = std::max(gsig, pipe ? 2 * gpair : gpair);
-  JW_HIP_TRY(hipMallocAsync((void**)&X, (size_t)batch * N * sizeof(cplx), s));
-  JW_HIP_TRY(hipMallocAsync((void**)&A, (size_t)a_items * N * sizeof(cplx), s));
+  JW_HIP_TRY(mem.alloc(&X, (size_t)batch * N * sizeof(cplx)));
+  JW_HIP_TRY(mem.alloc(&A, (size_t)a_items * N * sizeof(cplx)));
   // device scale table: [a_0 .. a_{ns-1} | (step, norm*sqrt(a)) per scale] (ScaleIn)
   std::vector<double> hsc(3 * (size_t)ns);
   for (int i = 0; i < ns; ++i) {
@@ -266,8 +267,8 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     hsc[ns + 2 * i + 1] = w.norm * std::sqrt(a);
   }
   w.p2 = wavelet == JW_CWT_MORLET ? -2.0 * kPi * kPi * w.p0 : -0.5 * w.p0 * w.p0;
-  JW_HIP_TRY(hipMallocAsync((void**)&dsc, hsc.size() * sizeof(double), s));
-  JW_HIP_TRY(hipMemcpyAsync(dsc, hsc.data(), hsc.size() * sizeof(double), hipMemcpyHostToDevice, s));
+  JW_HIP_TRY(mem.alloc(&dsc, hsc.size() * sizeof(double)));
+  JW_HIP_TRY(upload_async(dsc, hsc.data(), hsc.size() * sizeof(double), s));
   int logN = 0;
   while ((1L << logN) < N) ++logN;
   const long N1 = N <= 4096 ? N : 1L << ((logN + 1) / 2);
@@ -315,9 +316,6 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
       default: st = go(std::integral_constant<int, JW_CWT_MEYER>{}); break;
     }
   }
-  (void)hipFreeAsync(dsc, s);
-  (void)hipFreeAsync(A, s);
-  (void)hipFreeAsync(X, s);
   return st;
 }
 

@@ -236,12 +236,13 @@ int cwt_direct_device(int wavelet, const double* params, const double* x, long n
   double2* dtab = nullptr;
   long* doff = nullptr;
   int* dlohi = nullptr;
-  JW_HIP_TRY(hipMallocAsync((void**)&dtab, tab.size() * sizeof(double2), s));
-  JW_HIP_TRY(hipMallocAsync((void**)&doff, off.size() * sizeof(long), s));
-  JW_HIP_TRY(hipMallocAsync((void**)&dlohi, lohi.size() * sizeof(int), s));
-  JW_HIP_TRY(hipMemcpyAsync(dtab, tab.data(), tab.size() * sizeof(double2), hipMemcpyHostToDevice, s));
-  JW_HIP_TRY(hipMemcpyAsync(doff, off.data(), off.size() * sizeof(long), hipMemcpyHostToDevice, s));
-  JW_HIP_TRY(hipMemcpyAsync(dlohi, lohi.data(), lohi.size() * sizeof(int), hipMemcpyHostToDevice, s));
+  StreamAllocs mem(s);
+  JW_HIP_TRY(mem.alloc(&dtab, tab.size() * sizeof(double2)));
+  JW_HIP_TRY(mem.alloc(&doff, off.size() * sizeof(long)));
+  JW_HIP_TRY(mem.alloc(&dlohi, lohi.size() * sizeof(int)));
+  JW_HIP_TRY(upload_async(dtab, tab.data(), tab.size() * sizeof(double2), s));
+  JW_HIP_TRY(upload_async(doff, off.data(), off.size() * sizeof(long), s));
+  JW_HIP_TRY(upload_async(dlohi, lohi.data(), lohi.size() * sizeof(int), s));
   int st = JW_OK;
   for (int b0 = 0; b0 < batch; b0 += 65535) {
     const int nb = std::min(65535, batch - b0);
@@ -254,9 +255,6 @@ int cwt_direct_device(int wavelet, const double* params, const double* x, long n
                          doff, dlohi, ns, dt, out + (long)b0 * ns * n * 2);
     if (hipGetLastError() != hipSuccess) st = fail(JW_ERR_DEVICE, "direct CWT launch failed");
   }
-  (void)hipFreeAsync(dlohi, s);
-  (void)hipFreeAsync(doff, s);
-  (void)hipFreeAsync(dtab, s);
   return st;
 }
 

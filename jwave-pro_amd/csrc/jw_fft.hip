@@ -2,6 +2,7 @@
 #include <cmath>
 #include <map>
 #include <mutex>
+#include <utility>
 
 #include "jw_fft.hpp"
 
@@ -10,7 +11,10 @@ namespace fft {
 
 namespace {
 std::mutex g_mu;
-std::map<long, Tables> g_tables;  // per N, device memory owned for the library's lifetime
+// per (device, N): device memory owned for the library's lifetime.  Keyed by the calling
+// thread's current device, so one process driving several GPUs (a JVM with a thread per
+// GPU) never hands one device's tables to another.
+std::map<std::pair<int, long>, Tables> g_tables;
 
 void fill(cplx* h, long n, long N, long stride) {
   const long double two_pi = 6.283185307179586476925286766559005768L;
@@ -22,8 +26,11 @@ void fill(cplx* h, long n, long N, long stride) {
 }  // namespace
 
 int tables(long N, Tables* out) {
+  int dev = 0;
+  JW_HIP_TRY(hipGetDevice(&dev));
+  const std::pair<int, long> key(dev, N);
   std::lock_guard<std::mutex> lk(g_mu);
-  auto it = g_tables.find(N);
+  auto it = g_tables.find(key);
   if (it != g_tables.end()) {
     *out = it->second;
     return JW_OK;
@@ -51,7 +58,7 @@ int tables(long N, Tables* out) {
   t.w512 = d;
   t.lo = d + 512;
   t.hi = d + 512 + Q;
-  g_tables[N] = t;
+  g_tables[key] = t;
   *out = t;
   return JW_OK;
 }

@@ -944,7 +944,8 @@ int forward_t(const FwtPlan& p, const double* x, double* y, long n, int level, l
     return JW_OK;
   }
   double* tmp = nullptr;
-  JW_HIP_TRY(hipMallocAsync((void**)&tmp, sizeof(double) * (size_t)(n * batch), s));
+  StreamAllocs mem(s);
+  JW_HIP_TRY(mem.alloc(&tmp, sizeof(double) * (size_t)(n * batch)));
   if (y != x) JW_HIP_TRY(hipMemcpyAsync(y, x, sizeof(double) * n * batch, hipMemcpyDeviceToDevice, s));
   int l = 0;
   for (long h = n; h >= p.tw && l < level; h >>= 1, ++l) {
@@ -958,7 +959,6 @@ int forward_t(const FwtPlan& p, const double* x, double* y, long n, int level, l
                                 sizeof(double) * h, batch, hipMemcpyDeviceToDevice, s));
   }
   JW_HIP_TRY(hipGetLastError());
-  JW_HIP_TRY(hipFreeAsync(tmp, s));
   return JW_OK;
 }
 
@@ -983,7 +983,8 @@ int reverse_t(const FwtPlan& p, const double* y, double* x, long n, int level, l
     return JW_OK;
   }
   double* tmp = nullptr;
-  JW_HIP_TRY(hipMallocAsync((void**)&tmp, sizeof(double) * (size_t)(n * batch), s));
+  StreamAllocs mem(s);
+  JW_HIP_TRY(mem.alloc(&tmp, sizeof(double) * (size_t)(n * batch)));
   if (x != y) JW_HIP_TRY(hipMemcpyAsync(x, y, sizeof(double) * n * batch, hipMemcpyDeviceToDevice, s));
   for (long h = h0; h <= n && h >= p.tw; h <<= 1) {
     for (long b0 = 0; b0 < batch; b0 += 65535) {
@@ -996,7 +997,6 @@ int reverse_t(const FwtPlan& p, const double* y, double* x, long n, int level, l
                                 sizeof(double) * h, batch, hipMemcpyDeviceToDevice, s));
   }
   JW_HIP_TRY(hipGetLastError());
-  JW_HIP_TRY(hipFreeAsync(tmp, s));
   return JW_OK;
 }
 
@@ -1067,7 +1067,8 @@ int wpt_t(const FwtPlan& p, bool rev, const double* in, double* out, long n, int
   }
   // per-level global kernels, ping-pong between out and a workspace
   double* tmp = nullptr;
-  JW_HIP_TRY(hipMallocAsync((void**)&tmp, sizeof(double) * (size_t)(n * batch), s));
+  StreamAllocs mem(s);
+  JW_HIP_TRY(mem.alloc(&tmp, sizeof(double) * (size_t)(n * batch)));
   if (out != in) JW_HIP_TRY(hipMemcpyAsync(out, in, sizeof(double) * n * batch, hipMemcpyDeviceToDevice, s));
   double *a = out, *b = tmp;
   int l = 0;
@@ -1092,7 +1093,6 @@ int wpt_t(const FwtPlan& p, bool rev, const double* in, double* out, long n, int
   if (a != out)
     JW_HIP_TRY(hipMemcpyAsync(out, a, sizeof(double) * n * batch, hipMemcpyDeviceToDevice, s));
   JW_HIP_TRY(hipGetLastError());
-  JW_HIP_TRY(hipFreeAsync(tmp, s));
   return JW_OK;
 }
 
@@ -1138,8 +1138,9 @@ int fwt2d_forward_strips(const FwtPlan& p, int S, const double* x, double* y, in
                          int lvlM, int lvlN, int batch, hipStream_t s) {
   const long mat = (long)rows * cols, half = mat / 2;
   double *T = nullptr, *B = nullptr;
-  JW_HIP_TRY(hipMallocAsync((void**)&T, sizeof(double) * mat * batch, s));
-  JW_HIP_TRY(hipMallocAsync((void**)&B, sizeof(double) * half * batch, s));
+  StreamAllocs mem(s);
+  JW_HIP_TRY(mem.alloc(&T, sizeof(double) * mat * batch));
+  JW_HIP_TRY(mem.alloc(&B, sizeof(double) * half * batch));
   int st = fwt_forward_device(p, x, T, cols, lvlN, rows * batch, s);  // rows -> T
   const Filters f = make_filters(p);
   const int tail_lv = lvlM - S;
@@ -1159,8 +1160,6 @@ int fwt2d_forward_strips(const FwtPlan& p, int S, const double* x, double* y, in
                         p.tw, batch, f))
     st = fail(JW_ERR_UNSUPPORTED, "no 2-D strip kernel for filter length %d", p.M);
   if (st == JW_OK) JW_HIP_TRY(hipGetLastError());
-  (void)hipFreeAsync(B, s);
-  (void)hipFreeAsync(T, s);
   return st;
 }
 
@@ -1169,8 +1168,9 @@ int fwt2d_reverse_strips(const FwtPlan& p, int S, const double* y, double* x, in
                          int lvlM, int lvlN, int batch, hipStream_t s) {
   const long mat = (long)rows * cols, half = mat / 2;
   double *T = nullptr, *B = nullptr;
-  JW_HIP_TRY(hipMallocAsync((void**)&T, sizeof(double) * mat * batch, s));
-  JW_HIP_TRY(hipMallocAsync((void**)&B, sizeof(double) * half * batch, s));
+  StreamAllocs mem(s);
+  JW_HIP_TRY(mem.alloc(&T, sizeof(double) * mat * batch));
+  JW_HIP_TRY(mem.alloc(&B, sizeof(double) * half * batch));
   const Filters f = make_filters(p);
   const int tail_lv = lvlM - S;
   // level l (h = rows >> l) writes rows [0, h) of O_l: O_0 = T, then alternating with B
@@ -1197,8 +1197,6 @@ int fwt2d_reverse_strips(const FwtPlan& p, int S, const double* y, double* x, in
   }
   if (st == JW_OK) JW_HIP_TRY(hipGetLastError());
   if (st == JW_OK) st = fwt_reverse_device(p, T, x, cols, lvlN, rows * batch, s);  // rows
-  (void)hipFreeAsync(B, s);
-  (void)hipFreeAsync(T, s);
   return st;
 }
 
@@ -1230,21 +1228,21 @@ int fwt2d_forward_device(const FwtPlan& p, const double* x, double* y, int rows,
     // no fused kernel for this M: finish with the transpose path on y
     const size_t elems = (size_t)rows * cols * batch;
     double* t = nullptr;
-    JW_HIP_TRY(hipMallocAsync((void**)&t, sizeof(double) * elems, s));
+    StreamAllocs mem(s);
+    JW_HIP_TRY(mem.alloc(&t, sizeof(double) * elems));
     st = transpose(y, t, rows, cols, batch, s);
     if (st == JW_OK) st = fwt_forward_device(p, t, t, rows, lvlM, cols * batch, s);
     if (st == JW_OK) st = transpose(t, y, cols, rows, batch, s);
-    JW_HIP_TRY(hipFreeAsync(t, s));
     return st;
   }
   const size_t elems = (size_t)rows * cols * batch;
   double* t = nullptr;
-  JW_HIP_TRY(hipMallocAsync((void**)&t, sizeof(double) * elems, s));
+  StreamAllocs mem(s);
+  JW_HIP_TRY(mem.alloc(&t, sizeof(double) * elems));
   int st = fwt_forward_device(p, x, y, cols, lvlN, rows * batch, s);
   if (st == JW_OK) st = transpose(y, t, rows, cols, batch, s);
   if (st == JW_OK) st = fwt_forward_device(p, t, t, rows, lvlM, cols * batch, s);
   if (st == JW_OK) st = transpose(t, y, cols, rows, batch, s);
-  JW_HIP_TRY(hipFreeAsync(t, s));
   return st;
 }
 
@@ -1272,12 +1270,12 @@ int fwt2d_reverse_device(const FwtPlan& p, const double* y, double* x, int rows,
   }
   const size_t elems = (size_t)rows * cols * batch;
   double* t = nullptr;
-  JW_HIP_TRY(hipMallocAsync((void**)&t, sizeof(double) * elems, s));
+  StreamAllocs mem(s);
+  JW_HIP_TRY(mem.alloc(&t, sizeof(double) * elems));
   int st = transpose(y, t, rows, cols, batch, s);
   if (st == JW_OK) st = fwt_reverse_device(p, t, t, rows, lvlM, cols * batch, s);
   if (st == JW_OK) st = transpose(t, x, cols, rows, batch, s);
   if (st == JW_OK) st = fwt_reverse_device(p, x, x, cols, lvlN, rows * batch, s);
-  JW_HIP_TRY(hipFreeAsync(t, s));
   return st;
 }
 
@@ -1319,13 +1317,13 @@ int fwt_columns(const FwtPlan& p, bool rev, const double* in, double* out, int r
     }
   }
   double* t = nullptr;
-  JW_HIP_TRY(hipMallocAsync((void**)&t, sizeof(double) * elems, s));
+  StreamAllocs mem(s);
+  JW_HIP_TRY(mem.alloc(&t, sizeof(double) * elems));
   int st = transpose(in, t, rows, (int)cols, batch, s);
   if (st == JW_OK)
     st = rev ? fwt_reverse_device(p, t, t, rows, lvl, (int)(cols * batch), s)
              : fwt_forward_device(p, t, t, rows, lvl, (int)(cols * batch), s);
   if (st == JW_OK) st = transpose(t, out, (int)cols, rows, batch, s);
-  JW_HIP_TRY(hipFreeAsync(t, s));
   return st;
 }
 }  // namespace

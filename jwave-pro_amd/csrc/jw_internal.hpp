@@ -27,6 +27,42 @@ void clear_error();
                         __FILE__, __LINE__);                                               \
   } while (0)
 
+// Stream-ordered device allocations of one call, released on every exit path (the early
+// returns of JW_HIP_TRY included): hipFreeAsync on the call's stream, so the memory is
+// reused only after the work queued on that stream has consumed it.
+class StreamAllocs {
+ public:
+  explicit StreamAllocs(hipStream_t s) : s_(s) {}
+  StreamAllocs(const StreamAllocs&) = delete;
+  StreamAllocs& operator=(const StreamAllocs&) = delete;
+  ~StreamAllocs() {
+    for (int i = n_ - 1; i >= 0; --i) (void)hipFreeAsync(p_[i], s_);
+  }
+  template <class T>
+  hipError_t alloc(T** out, size_t bytes) {
+    *out = nullptr;
+    if (n_ == kMax) return hipErrorOutOfMemory;
+    void* p = nullptr;
+    const hipError_t e = hipMallocAsync(&p, bytes, s_);
+    if (e == hipSuccess) {
+      p_[n_++] = p;
+      *out = (T*)p;
+    }
+    return e;
+  }
+
+ private:
+  static constexpr int kMax = 16;
+  hipStream_t s_;
+  void* p_[kMax] = {};
+  int n_ = 0;
+};
+
+// Host -> device copy that stays asynchronous: the bytes are copied into a heap buffer that
+// a host callback on the stream frees once the transfer has been reached (the caller's
+// buffer may go away as soon as this returns).
+hipError_t upload_async(void* dst, const void* src, size_t bytes, hipStream_t s);
+
 // Filter taps passed to kernels by value (lands in SGPRs: wave-uniform).
 struct Taps {
   double a[kMaxTaps];
@@ -60,6 +96,9 @@ int modwt_forward_fft_device(const ModwtPlan& p, const double* x, double* coeffs
                              int batch, hipStream_t s);
 int modwt_inverse_fft_device(const ModwtPlan& p, const double* coeffs, double* x, long n, int J,
                              int batch, hipStream_t s);
+// FastFourierTransform.forward (S = -1) / reverse (S = +1, scaled by 1/n) of batch lines of n
+// interleaved complex values in HBM; in == out allowed.
+int fft_device(int S, const double* in, double* out, long n, long batch, hipStream_t s);
 int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
                    const double* scales_host, int ns, double fs, int padding, double* out,
                    int batch, hipStream_t s);
@@ -87,8 +126,5 @@ int fwt3d_forward_device(const FwtPlan& p, const double* x, double* y, int R, in
 int fwt3d_reverse_device(const FwtPlan& p, const double* y, double* x, int R, int C, int H,
                          int lvlP, int lvlQ, int lvlR, int batch, hipStream_t s);
 int synth_uniform_device(double* x, long n, int batch, long seed0, hipStream_t s);
-
-// Device workspace that grows on demand (per calling thread, per device).
-double* workspace(size_t doubles, int* status);
 
 }  // namespace jw

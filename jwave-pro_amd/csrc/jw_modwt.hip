@@ -474,7 +474,8 @@ int forward_impl(const ModwtPlan& p, const double* x, double* coeffs, long N, in
   // Per-level path: V_j ping-pongs between coefficient row J and a workspace row so that
   // V_J lands in row J.
   double* tmp = nullptr;
-  JW_HIP_TRY(hipMallocAsync((void**)&tmp, sizeof(double) * (size_t)N * batch, s));
+  StreamAllocs mem(s);
+  JW_HIP_TRY(mem.alloc(&tmp, sizeof(double) * (size_t)N * batch));
   const double* vin = x;
   long vin_stride = N;
   for (int j = 1; j <= J; ++j) {
@@ -492,7 +493,6 @@ int forward_impl(const ModwtPlan& p, const double* x, double* coeffs, long N, in
     vin = vout;
     vin_stride = vout_stride;
   }
-  JW_HIP_TRY(hipFreeAsync(tmp, s));
   return JW_OK;
 }
 
@@ -521,7 +521,8 @@ int inverse_impl(const ModwtPlan& p, const double* coeffs, double* x, long N, in
     return JW_OK;
   }
   double* tmp = nullptr;
-  JW_HIP_TRY(hipMallocAsync((void**)&tmp, sizeof(double) * (size_t)N * batch, s));
+  StreamAllocs mem(s);
+  JW_HIP_TRY(mem.alloc(&tmp, sizeof(double) * (size_t)N * batch));
   const double* vin = coeffs + (long)J * N;
   long vin_stride = rstride;
   for (int j = J; j >= 1; --j) {
@@ -538,7 +539,6 @@ int inverse_impl(const ModwtPlan& p, const double* coeffs, double* x, long N, in
     vin = vout;
     vin_stride = N;
   }
-  JW_HIP_TRY(hipFreeAsync(tmp, s));
   return JW_OK;
 }
 

@@ -99,7 +99,7 @@ struct InvIn {
   }
 };
 
-int prepare(long N, const ModwtPlan& p, Tables* T, cplx** R, hipStream_t s) {
+int prepare(long N, const ModwtPlan& p, Tables* T, cplx** R, StreamAllocs& mem, hipStream_t s) {
   int st = fft::tables(N, T);
   if (st != JW_OK) return st;
   Taps taps;
@@ -107,7 +107,7 @@ int prepare(long N, const ModwtPlan& p, Tables* T, cplx** R, hipStream_t s) {
     taps.a[m] = p.g[m];
     taps.b[m] = p.h[m];
   }
-  JW_HIP_TRY(hipMallocAsync((void**)R, (size_t)2 * N * sizeof(cplx), s));
+  JW_HIP_TRY(mem.alloc(R, (size_t)2 * N * sizeof(cplx)));
   hipLaunchKernelGGL(filter_response, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, *R,
                      taps, p.L, N, *T);
   JW_HIP_TRY(hipGetLastError());
@@ -185,7 +185,7 @@ struct Bluestein {
   cplx* bh[2] = {};        // FFT_M(b) for S = -1 (index 0) and S = +1 (index 1)
   cplx* ws = nullptr;      // 2 x items x M workspace
   long ws_items = 0;
-};
+};  // device buffers owned by the caller's StreamAllocs
 
 unsigned blocks(long n) { return (unsigned)((n + 255) / 256); }
 
@@ -198,7 +198,7 @@ int fft_natural(int S, long M, long items, const cplx* in, cplx* out, cplx* A, h
                                  A, s, T, false);
 }
 
-int bluestein_init(Bluestein* B, long N, long max_items, hipStream_t s) {
+int bluestein_init(Bluestein* B, long N, long max_items, StreamAllocs& mem, hipStream_t s) {
   B->N = N;
   B->M = 1;
   while (B->M < 2 * N - 1) B->M <<= 1;
@@ -213,11 +213,11 @@ int bluestein_init(Bluestein* B, long N, long max_items, hipStream_t s) {
     hw[n] = make_double2((double)cosl(ang), (double)sinl(ang));
   }
   B->ws_items = max_items;
-  JW_HIP_TRY(hipMallocAsync((void**)&B->w, N * sizeof(cplx), s));
-  JW_HIP_TRY(hipMallocAsync((void**)&B->bh[0], 2 * M * sizeof(cplx), s));
+  JW_HIP_TRY(mem.alloc(&B->w, N * sizeof(cplx)));
+  JW_HIP_TRY(mem.alloc(&B->bh[0], 2 * M * sizeof(cplx)));
   B->bh[1] = B->bh[0] + M;
-  JW_HIP_TRY(hipMallocAsync((void**)&B->ws, (size_t)2 * max_items * M * sizeof(cplx), s));
-  JW_HIP_TRY(hipMemcpyAsync(B->w, hw.data(), N * sizeof(cplx), hipMemcpyHostToDevice, s));
+  JW_HIP_TRY(mem.alloc(&B->ws, (size_t)2 * max_items * M * sizeof(cplx)));
+  JW_HIP_TRY(upload_async(B->w, hw.data(), N * sizeof(cplx), s));
   // b_m for both signs, then their FFTs (two items of length M)
   std::vector<cplx> hb(2 * M, make_double2(0.0, 0.0));
   for (int q = 0; q < 2; ++q) {  // q = 0: S = -1 -> b = c; q = 1: S = +1 -> b = conj(c)
@@ -228,18 +228,9 @@ int bluestein_init(Bluestein* B, long N, long max_items, hipStream_t s) {
     }
   }
   cplx* tmp = B->ws;  // the workspace's first 2M entries stage b
-  JW_HIP_TRY(hipMemcpyAsync(tmp, hb.data(), 2 * M * sizeof(cplx), hipMemcpyHostToDevice, s));
+  JW_HIP_TRY(upload_async(tmp, hb.data(), 2 * M * sizeof(cplx), s));
   // pass workspace: the next 2M entries (ws holds 2 x max_items x M, max_items = batch (J+1) >= 2)
-  st = fft_natural(-1, M, 2, tmp, B->bh[0], B->ws + 2 * M, s, B->T);
-  if (st != JW_OK) return st;
-  JW_HIP_TRY(hipStreamSynchronize(s));  // hw / hb are host locals
-  return JW_OK;
-}
-
-void bluestein_free(Bluestein* B, hipStream_t s) {
-  (void)hipFreeAsync(B->ws, s);
-  (void)hipFreeAsync(B->bh[0], s);
-  (void)hipFreeAsync(B->w, s);
+  return fft_natural(-1, M, 2, tmp, B->bh[0], B->ws + 2 * M, s, B->T);
 }
 
 // items length-N DFTs (S = -1 forward, +1 reverse without 1/N), natural order in -> out
@@ -319,13 +310,13 @@ __global__ void inv_combine(const cplx* __restrict__ C, const cplx* __restrict__
   Sout[i] = sv;
 }
 
-int prepare_any(long N, const ModwtPlan& p, cplx** R, hipStream_t s) {
+int prepare_any(long N, const ModwtPlan& p, cplx** R, StreamAllocs& mem, hipStream_t s) {
   Taps taps;
   for (int m = 0; m < p.L; ++m) {
     taps.a[m] = p.g[m];
     taps.b[m] = p.h[m];
   }
-  JW_HIP_TRY(hipMallocAsync((void**)R, (size_t)2 * N * sizeof(cplx), s));
+  JW_HIP_TRY(mem.alloc(R, (size_t)2 * N * sizeof(cplx)));
   hipLaunchKernelGGL(filter_response_any, dim3(blocks(N)), dim3(256), 0, s, *R, taps, p.L, N);
   JW_HIP_TRY(hipGetLastError());
   return JW_OK;
@@ -339,19 +330,19 @@ long chunk_any(long N, long M, int J, int batch) {
 
 int forward_any(const ModwtPlan& p, const double* x, double* coeffs, long N, int J, int batch,
                 hipStream_t s) {
+  StreamAllocs mem(s);
   cplx* R = nullptr;
-  int st = prepare_any(N, p, &R, s);
+  int st = prepare_any(N, p, &R, mem, s);
   if (st != JW_OK) return st;
   long M = 1;
   while (M < 2 * N - 1) M <<= 1;
   const long bc = chunk_any(N, M, J, batch);
   Bluestein B;
-  st = bluestein_init(&B, N, bc * (J + 1), s);
+  st = bluestein_init(&B, N, bc * (J + 1), mem, s);
+  if (st != JW_OK) return st;
   cplx *X = nullptr, *Y = nullptr;
-  if (st == JW_OK) {
-    JW_HIP_TRY(hipMallocAsync((void**)&X, (size_t)bc * N * sizeof(cplx), s));
-    JW_HIP_TRY(hipMallocAsync((void**)&Y, (size_t)bc * (J + 1) * N * sizeof(cplx), s));
-  }
+  JW_HIP_TRY(mem.alloc(&X, (size_t)bc * N * sizeof(cplx)));
+  JW_HIP_TRY(mem.alloc(&Y, (size_t)bc * (J + 1) * N * sizeof(cplx)));
   for (long b0 = 0; b0 < batch && st == JW_OK; b0 += bc) {
     const long nb = std::min<long>(bc, batch - b0);
     hipLaunchKernelGGL(real_to_cplx, dim3(blocks(nb * N)), dim3(256), 0, s, x + b0 * N, Y, nb * N);
@@ -364,28 +355,24 @@ int forward_any(const ModwtPlan& p, const double* x, double* coeffs, long N, int
                        coeffs + b0 * (long)(J + 1) * N, nb * (J + 1) * N, 1.0 / (double)N);
     JW_HIP_TRY(hipGetLastError());
   }
-  (void)hipFreeAsync(Y, s);
-  (void)hipFreeAsync(X, s);
-  bluestein_free(&B, s);
-  (void)hipFreeAsync(R, s);
   return st;
 }
 
 int inverse_any(const ModwtPlan& p, const double* coeffs, double* x, long N, int J, int batch,
                 hipStream_t s) {
+  StreamAllocs mem(s);
   cplx* R = nullptr;
-  int st = prepare_any(N, p, &R, s);
+  int st = prepare_any(N, p, &R, mem, s);
   if (st != JW_OK) return st;
   long M = 1;
   while (M < 2 * N - 1) M <<= 1;
   const long bc = chunk_any(N, M, J, batch);
   Bluestein B;
-  st = bluestein_init(&B, N, bc * (J + 1), s);
+  st = bluestein_init(&B, N, bc * (J + 1), mem, s);
+  if (st != JW_OK) return st;
   cplx *C = nullptr, *S = nullptr;
-  if (st == JW_OK) {
-    JW_HIP_TRY(hipMallocAsync((void**)&C, (size_t)bc * (J + 1) * N * sizeof(cplx), s));
-    JW_HIP_TRY(hipMallocAsync((void**)&S, (size_t)bc * N * sizeof(cplx), s));
-  }
+  JW_HIP_TRY(mem.alloc(&C, (size_t)bc * (J + 1) * N * sizeof(cplx)));
+  JW_HIP_TRY(mem.alloc(&S, (size_t)bc * N * sizeof(cplx)));
   for (long b0 = 0; b0 < batch && st == JW_OK; b0 += bc) {
     const long nb = std::min<long>(bc, batch - b0);
     hipLaunchKernelGGL(real_to_cplx, dim3(blocks(nb * (J + 1) * N)), dim3(256), 0, s,
@@ -399,14 +386,81 @@ int inverse_any(const ModwtPlan& p, const double* coeffs, double* x, long N, int
                        nb * N, 1.0 / (double)N);
     JW_HIP_TRY(hipGetLastError());
   }
-  (void)hipFreeAsync(S, s);
-  (void)hipFreeAsync(C, s);
-  bluestein_free(&B, s);
-  (void)hipFreeAsync(R, s);
   return st;
 }
 
+// FastFourierTransform.forward/reverse(Complex[]) front-end (jw_fft_forward / jw_fft_reverse):
+// natural-order interleaved lines, the reverse scaled by 1/n (:207-211).
+struct NatOut1S {  // single pass: out[item][idx] * scale
+  cplx* o;
+  long M;
+  double scale;
+  __device__ void operator()(long item, long idx, long, cplx v) const {
+    o[item * M + idx] = make_double2(v.x * scale, v.y * scale);
+  }
+};
+struct NatOutS {  // four-step: out[item][n1 + N1 n2] * scale
+  cplx* o;
+  long M, N1;
+  double scale;
+  __device__ void operator()(long item, long idx, long line, cplx v) const {
+    o[item * M + line + N1 * idx] = make_double2(v.x * scale, v.y * scale);
+  }
+};
+__global__ void cplx_scale(cplx* __restrict__ a, long n, double f) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) a[i] = make_double2(a[i].x * f, a[i].y * f);
+}
+
 }  // namespace
+
+int fft_device(int S, const double* in, double* out, long n, long batch, hipStream_t s) {
+  if (n == 0 || batch == 0) return JW_OK;
+  const cplx* x = (const cplx*)in;
+  cplx* y = (cplx*)out;
+  if (n == 1) {  // forward/reverse return a copy (:117-119, :146-148)
+    if (in != out) JW_HIP_TRY(hipMemcpyAsync(out, in, (size_t)batch * sizeof(cplx),
+                                             hipMemcpyDeviceToDevice, s));
+    return JW_OK;
+  }
+  StreamAllocs mem(s);
+  if ((n & (n - 1)) == 0) {  // Cooley-Tukey lengths: the four-step engine (exact twiddles)
+    Tables T;
+    int st = fft::tables(n, &T);
+    if (st != JW_OK) return st;
+    const long N1 = fft::split_n1(n), N2 = n / N1;
+    const double scale = S > 0 ? 1.0 / (double)n : 1.0;
+    // lines per launch: grid y <= 32768 and a pass workspace of at most 512 MiB
+    const long chunk = std::max(1L, std::min<long>({batch, 32768L,
+                                                   (512L << 20) / (n * (long)sizeof(cplx))}));
+    cplx* A = nullptr;
+    if (n > 4096) JW_HIP_TRY(mem.alloc(&A, (size_t)chunk * n * sizeof(cplx)));
+    for (long b0 = 0; b0 < batch && st == JW_OK; b0 += chunk) {
+      const long nb = std::min(chunk, batch - b0);
+      const NatIn fin{x + b0 * n, n, N2};
+      const NatOut1S o1{y + b0 * n, n, scale};
+      const NatOutS o2{y + b0 * n, n, N1, scale};
+      st = S < 0 ? fft::run_fft<-1>(n, nb, fin, o1, o2, A, s, T, false)
+                 : fft::run_fft<1>(n, nb, fin, o1, o2, A, s, T, false);
+    }
+    return st;
+  }
+  // Bluestein lengths (:259-324): the chirp-z transform over the power-of-two engine
+  if (n > (1L << 23)) return fail(JW_ERR_UNSUPPORTED, "FFT length %ld > 2^23 (not a power of 2)", n);
+  long M = 1;
+  while (M < 2 * n - 1) M <<= 1;
+  const long items = std::max(2L, std::min<long>(batch, (1L << 30) / (2 * M * (long)sizeof(cplx))));
+  Bluestein B;
+  int st = bluestein_init(&B, n, items, mem, s);
+  if (st != JW_OK) return st;
+  st = bluestein_dft(B, S < 0 ? -1 : 1, batch, x, y, s);
+  if (st == JW_OK && S > 0) {
+    hipLaunchKernelGGL(cplx_scale, dim3(blocks(batch * n)), dim3(256), 0, s, y, batch * n,
+                       1.0 / (double)n);
+    JW_HIP_TRY(hipGetLastError());
+  }
+  return st;
+}
 
 static bool is_pow2(long N) { return (N & (N - 1)) == 0; }
 
@@ -416,15 +470,16 @@ bool modwt_fft_supported(long N) { return N >= 2 && N <= (1L << 23); }
 int modwt_forward_fft_device(const ModwtPlan& p, const double* x, double* coeffs, long N, int J,
                              int batch, hipStream_t s) {
   if (!is_pow2(N)) return forward_any(p, x, coeffs, N, J, batch, s);
+  StreamAllocs mem(s);
   Tables T;
   cplx* R = nullptr;
-  int st = prepare(N, p, &T, &R, s);
+  int st = prepare(N, p, &T, &R, mem, s);
   if (st != JW_OK) return st;
   const long N1 = fft::split_n1(N), N2 = N / N1;
   const long bc = chunk_signals(N, J, batch);
   cplx *X = nullptr, *A = nullptr;
-  JW_HIP_TRY(hipMallocAsync((void**)&X, (size_t)bc * N * sizeof(cplx), s));
-  JW_HIP_TRY(hipMallocAsync((void**)&A, (size_t)bc * (J + 1) * N * sizeof(cplx), s));
+  JW_HIP_TRY(mem.alloc(&X, (size_t)bc * N * sizeof(cplx)));
+  JW_HIP_TRY(mem.alloc(&A, (size_t)bc * (J + 1) * N * sizeof(cplx)));
   for (long b0 = 0; b0 < batch && st == JW_OK; b0 += bc) {
     const long nb = std::min<long>(bc, batch - b0);
     st = fft::run_fft<-1>(N, nb, RealIn{x + b0 * N, N, N2}, fft::SpecOut1{X, N, 0},
@@ -435,24 +490,22 @@ int modwt_forward_fft_device(const ModwtPlan& p, const double* x, double* coeffs
     st = fft::run_fft<1>(N, nb * (J + 1), FwdIn{X, R, N, N1, N2, J}, RealOut{o, N, 1, inv},
                          RealOut{o, N, N1, inv}, A, s, T, false);
   }
-  (void)hipFreeAsync(A, s);
-  (void)hipFreeAsync(X, s);
-  (void)hipFreeAsync(R, s);
   return st;
 }
 
 int modwt_inverse_fft_device(const ModwtPlan& p, const double* coeffs, double* x, long N, int J,
                              int batch, hipStream_t s) {
   if (!is_pow2(N)) return inverse_any(p, coeffs, x, N, J, batch, s);
+  StreamAllocs mem(s);
   Tables T;
   cplx* R = nullptr;
-  int st = prepare(N, p, &T, &R, s);
+  int st = prepare(N, p, &T, &R, mem, s);
   if (st != JW_OK) return st;
   const long N1 = fft::split_n1(N), N2 = N / N1;
   const long bc = chunk_signals(N, J, batch);
   cplx *C = nullptr, *A = nullptr;
-  JW_HIP_TRY(hipMallocAsync((void**)&C, (size_t)bc * (J + 1) * N * sizeof(cplx), s));
-  JW_HIP_TRY(hipMallocAsync((void**)&A, (size_t)bc * (J + 1) * N * sizeof(cplx), s));
+  JW_HIP_TRY(mem.alloc(&C, (size_t)bc * (J + 1) * N * sizeof(cplx)));
+  JW_HIP_TRY(mem.alloc(&A, (size_t)bc * (J + 1) * N * sizeof(cplx)));
   for (long b0 = 0; b0 < batch && st == JW_OK; b0 += bc) {
     const long nb = std::min<long>(bc, batch - b0);
     st = fft::run_fft<-1>(N, nb * (J + 1), RealIn{coeffs + b0 * (long)(J + 1) * N, N, N2},
@@ -462,9 +515,6 @@ int modwt_inverse_fft_device(const ModwtPlan& p, const double* coeffs, double* x
     st = fft::run_fft<1>(N, nb, InvIn{C, R, N, N1, N2, J}, RealOut{x + b0 * N, N, 1, inv},
                          RealOut{x + b0 * N, N, N1, inv}, A, s, T, false);
   }
-  (void)hipFreeAsync(A, s);
-  (void)hipFreeAsync(C, s);
-  (void)hipFreeAsync(R, s);
   return st;
 }
 

@@ -6,11 +6,11 @@ All compute goes through libjwave_hip.so (include/jwave_hip.h); there is no CPU 
 """
 from . import exceptions, transforms
 from .Transform import Transform
-from .transforms import (ContinuousWaveletTransform, FastWaveletTransform, MODWTTransform,
-                         WaveletPacketTransform)
+from .transforms import (ContinuousWaveletTransform, FastFourierTransform, FastWaveletTransform,
+                         MODWTTransform, WaveletPacketTransform)
 from .transforms import wavelets
 
 __version__ = "0.1.0"
 __all__ = ["Transform", "FastWaveletTransform", "MODWTTransform", "ContinuousWaveletTransform",
-           "WaveletPacketTransform",
+           "WaveletPacketTransform", "FastFourierTransform",
            "wavelets", "exceptions", "transforms"]

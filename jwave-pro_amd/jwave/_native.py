@@ -41,7 +41,8 @@ JW_ARITH_FMA = 1
 JW_WAVELET_GENERIC = 0
 JW_WAVELET_HAAR_ORTH = 1
 
-# Every symbol include/jwave_hip.h declares (checked by tests/test_capi_symbols.py).
+# Every symbol include/jwave_hip.h declares (checked by
+# tests/test_capi.py::test_library_exports_every_header_symbol).
 EXPORTS = (
     "jw_last_error", "jw_version",
     "jw_modwt_plan_create", "jw_modwt_plan_destroy", "jw_modwt_plan_filters",
@@ -49,6 +50,7 @@ EXPORTS = (
     "jw_fwt_plan_create", "jw_fwt_plan_destroy", "jw_fwt_forward", "jw_fwt_reverse",
     "jw_fwt2d_forward", "jw_fwt2d_reverse", "jw_fwt3d_forward", "jw_fwt3d_reverse",
     "jw_synth_uniform", "jw_cwt_fft", "jw_cwt_direct", "jw_wpt_forward", "jw_wpt_reverse",
+    "jw_fft_forward", "jw_fft_reverse",
 )
 
 _lib = None
@@ -96,6 +98,8 @@ def lib():
     L.jw_fwt3d_forward.argtypes = [c_dp, c_dp, c_dp, i, i, i, i, i, i, i, i, c_dp]
     L.jw_fwt3d_reverse.argtypes = [c_dp, c_dp, c_dp, i, i, i, i, i, i, i, i, c_dp]
     L.jw_synth_uniform.argtypes = [c_dp, l, i, l, c_dp]
+    L.jw_fft_forward.argtypes = [c_dp, c_dp, l, i, i, c_dp]
+    L.jw_fft_reverse.argtypes = [c_dp, c_dp, l, i, i, c_dp]
     L.jw_cwt_fft.argtypes = [i, c_dp, c_dp, l, c_dp, i, ctypes.c_double, i, c_dp, i, i, c_dp]
     L.jw_cwt_direct.argtypes = [i, c_dp, c_dp, l, c_dp, i, ctypes.c_double, i, c_dp, i, i, c_dp]
     non_int = ("jw_last_error", "jw_version", "jw_modwt_plan_destroy", "jw_fwt_plan_destroy")

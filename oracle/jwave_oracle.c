@@ -650,24 +650,206 @@ void jwo_cwt_fft(int wavelet, const double* params, const double* x, long n,
 }
 
 /* ------------------------------------------------------------------------ */
-/* CPU baseline: ForkJoin-equivalent parallel loop over the batch (OpenMP).        */
+/* CPU baselines: the reference's ForkJoin patterns restated with OpenMP tasks.      */
+/* RecursiveAction halving (ParallelTransform.java:222-335: split [lo, hi) in two    */
+/* while hi - lo > THRESHOLD, invokeAll, leaves run serially).                       */
 /* ------------------------------------------------------------------------ */
-void jwo_modwt_fwdinv_batch(const double* x, long N, int J, const double* g, const double* h,
-                            int L, int B, int use_fft, int threads, double* coeffs, double* xr) {
+typedef void (*jwo_range_fn)(long lo, long hi, void* ctx);
+
+static void fj_invoke(long lo, long hi, long leaf, jwo_range_fn fn, void* ctx) {
+  if (hi - lo <= leaf) {
+    fn(lo, hi, ctx);
+    return;
+  }
+  long mid = lo + (hi - lo) / 2;
+#pragma omp task firstprivate(lo, mid, leaf, fn, ctx)
+  fj_invoke(lo, mid, leaf, fn, ctx);
+  fj_invoke(mid, hi, leaf, fn, ctx);
+#pragma omp taskwait
+}
+
+/* ForkJoinPool.invoke: one pool of `threads` workers runs the whole task tree. */
+static void fj_pool(long n, long leaf, int threads, jwo_range_fn fn, void* ctx) {
+  if (leaf < 1) leaf = 1;
 #ifdef _OPENMP
   if (threads > 0) omp_set_num_threads(threads);
-#pragma omp parallel for schedule(dynamic, 1)
+#pragma omp parallel
+#pragma omp single
 #endif
-  for (int b = 0; b < B; b++) {
-    double* c = coeffs + (long)b * (J + 1) * N;
-    if (use_fft) {
-      jwo_modwt_forward_fft(x + (long)b * N, N, J, g, h, L, c);
-      jwo_modwt_inverse_fft(c, N, J, g, h, L, xr + (long)b * N);
+  fj_invoke(0, n, leaf, fn, ctx);
+}
+
+/* leaf size: the reference's THRESHOLD of 16, lowered when the bounded sample has fewer
+ * than 16 items per worker so every worker gets a leaf */
+static long fj_leaf(long n, int threads) {
+  long per = threads > 0 ? n / threads : n;
+  return per < 1 ? 1 : (per < 16 ? per : 16);
+}
+
+typedef struct {
+  const double *x, *g, *h;
+  long N;
+  int J, L, use_fft;
+  double *coeffs, *xr;
+} modwt_batch_ctx;
+
+static void modwt_batch_leaf(long lo, long hi, void* p) {
+  modwt_batch_ctx* c = (modwt_batch_ctx*)p;
+  for (long b = lo; b < hi; b++) {
+    double* cf = c->coeffs + b * (c->J + 1) * c->N;
+    if (c->use_fft) {
+      jwo_modwt_forward_fft(c->x + b * c->N, c->N, c->J, c->g, c->h, c->L, cf);
+      jwo_modwt_inverse_fft(cf, c->N, c->J, c->g, c->h, c->L, c->xr + b * c->N);
     } else {
-      jwo_modwt_forward_direct(x + (long)b * N, N, J, g, h, L, c);
-      jwo_modwt_inverse_direct(c, N, J, g, h, L, xr + (long)b * N);
+      jwo_modwt_forward_direct(c->x + b * c->N, c->N, c->J, c->g, c->h, c->L, cf);
+      jwo_modwt_inverse_direct(cf, c->N, c->J, c->g, c->h, c->L, c->xr + b * c->N);
     }
   }
+}
+
+/* MODWT over a batch of independent signals: forwardMODWT + inverseMODWT per signal
+ * (MODWTTransform.java:256-375), signals split by ForkJoin halving. */
+void jwo_modwt_fwdinv_batch(const double* x, long N, int J, const double* g, const double* h,
+                            int L, int B, int use_fft, int threads, double* coeffs, double* xr) {
+  modwt_batch_ctx c = {x, g, h, N, J, L, use_fft, coeffs, xr};
+  fj_pool(B, fj_leaf(B, threads), threads, modwt_batch_leaf, &c);
+}
+
+/* ParallelTransform 2-D (ParallelTransform.java:70-126): per matrix, pool.invoke(RowTransformTask)
+ * then pool.invoke(ColumnTransformTask) for the forward, columns then rows for the reverse;
+ * leaves of <= 16 rows / columns (THRESHOLD :28) run FastWaveletTransform 1-D per line. */
+typedef struct {
+  const double* src;
+  double* dst;
+  int rows, cols, lvl, fwd, M, tw, kind;
+  const double *f0, *f1;
+} fwt2d_ctx;
+
+static void fwt2d_rows_leaf(long lo, long hi, void* p) {
+  fwt2d_ctx* c = (fwt2d_ctx*)p;
+  for (long i = lo; i < hi; i++) {
+    if (c->fwd)
+      jwo_fwt_forward(c->src + i * c->cols, c->cols, c->lvl, c->f0, c->f1, c->M, c->tw,
+                      c->dst + i * c->cols);
+    else
+      jwo_fwt_reverse(c->src + i * c->cols, c->cols, c->lvl, c->f0, c->f1, c->M, c->tw, c->kind,
+                      c->dst + i * c->cols);
+  }
+}
+
+static void fwt2d_cols_leaf(long lo, long hi, void* p) {
+  fwt2d_ctx* c = (fwt2d_ctx*)p;
+  double* a = (double*)malloc(sizeof(double) * c->rows);
+  double* b = (double*)malloc(sizeof(double) * c->rows);
+  for (long j = lo; j < hi; j++) {
+    for (int i = 0; i < c->rows; i++) a[i] = c->src[(long)i * c->cols + j];
+    if (c->fwd)
+      jwo_fwt_forward(a, c->rows, c->lvl, c->f0, c->f1, c->M, c->tw, b);
+    else
+      jwo_fwt_reverse(a, c->rows, c->lvl, c->f0, c->f1, c->M, c->tw, c->kind, b);
+    for (int i = 0; i < c->rows; i++) c->dst[(long)i * c->cols + j] = b[i];
+  }
+  free(a);
+  free(b);
+}
+
+/* forward + reverse of B matrices (rows x cols): y = forward(x), xr = reverse(y) */
+void jwo_fwt2d_fwdrev_parallel(const double* x, int B, int rows, int cols, int lvlM, int lvlN,
+                               const double* sD, const double* wD, const double* sR,
+                               const double* wR, int M, int tw, int kind, int threads,
+                               double* y, double* xr) {
+  const long img = (long)rows * cols;
+  for (int b = 0; b < B; b++) {
+    fwt2d_ctx r = {x + b * img, y + b * img, rows, cols, lvlN, 1, M, tw, kind, sD, wD};
+    fj_pool(rows, 16, threads, fwt2d_rows_leaf, &r);
+    fwt2d_ctx c = {y + b * img, y + b * img, rows, cols, lvlM, 1, M, tw, kind, sD, wD};
+    fj_pool(cols, 16, threads, fwt2d_cols_leaf, &c);
+    fwt2d_ctx rc = {y + b * img, xr + b * img, rows, cols, lvlM, 0, M, tw, kind, sR, wR};
+    fj_pool(cols, 16, threads, fwt2d_cols_leaf, &rc);
+    fwt2d_ctx rr = {xr + b * img, xr + b * img, rows, cols, lvlN, 0, M, tw, kind, sR, wR};
+    fj_pool(rows, 16, threads, fwt2d_rows_leaf, &rr);
+  }
+}
+
+/* transformFFTParallel (ContinuousWaveletTransform.java:511-565) over a batch of signals:
+ * signals in the outer pool, per signal one FFT then the scales in parallel, each scale
+ * psi_hat conj x X -> IFFT -> first n samples.  Recurrence twiddles (the reference's FFT). */
+typedef struct {
+  int wavelet;
+  const double* params;
+  const double* x;
+  long n, np;
+  const double* scales;
+  int ns;
+  double fs;
+  int padding;
+  double* out;
+  /* per-signal state, set by the signal task */
+  const double* X;
+  const double* omega;
+  long sig;
+} cwt_ctx;
+
+static void cwt_scale_leaf(long lo, long hi, void* p) {
+  cwt_ctx* c = (cwt_ctx*)p;
+  double* P = (double*)malloc(sizeof(double) * 2 * c->np);
+  for (long s = lo; s < hi; s++) {
+    for (long i = 0; i < c->np; i++) {
+      double wr, wi;
+      jwo_cwt_wavelet_ft_c(c->wavelet, c->params, c->omega[i], c->scales[s], &wr, &wi);
+      wi = -wi;
+      double sr = c->X[2 * i], si = c->X[2 * i + 1];
+      P[2 * i] = sr * wr - si * wi;
+      P[2 * i + 1] = sr * wi + si * wr;
+    }
+    jwo_fft(P, c->np, 1);
+    memcpy(c->out + (c->sig * c->ns + s) * c->n * 2, P, sizeof(double) * 2 * c->n);
+  }
+  free(P);
+}
+
+static void cwt_signal_leaf(long lo, long hi, void* p) {
+  const cwt_ctx* c0 = (const cwt_ctx*)p;
+  for (long b = lo; b < hi; b++) {
+    const long n = c0->n, np = c0->np;
+    const double* x = c0->x + b * n;
+    double* X = (double*)calloc(2 * np, sizeof(double));
+    for (long i = 0; i < n; i++) X[2 * i] = x[i];
+    for (long i = n; i < np; i++) { /* padSignal :269-306 */
+      double v = 0.0;
+      if (c0->padding == 1) {
+        long mi = 2 * n - i - 2;
+        if (mi >= 0 && mi < n) v = x[mi];
+      } else if (c0->padding == 2) {
+        v = x[i % n];
+      } else if (c0->padding == 3) {
+        v = x[n - 1];
+      }
+      X[2 * i] = v;
+    }
+    jwo_fft(X, np, 0);
+    double* omega = (double*)malloc(sizeof(double) * np);
+    for (long i = 0; i < np; i++) {
+      omega[i] = 2.0 * JAVA_PI * (double)i * c0->fs / (double)np;
+      if (i > np / 2) omega[i] -= 2.0 * JAVA_PI * c0->fs;
+    }
+    cwt_ctx c = *c0;
+    c.X = X;
+    c.omega = omega;
+    c.sig = b;
+    fj_invoke(0, c.ns, 1, cwt_scale_leaf, &c); /* IntStream.range(0, nScales).parallel() */
+    free(omega);
+    free(X);
+  }
+}
+
+void jwo_cwt_fft_parallel_batch(int wavelet, const double* params, const double* x, long n,
+                                const double* scales, int ns, double fs, int padding, int B,
+                                int threads, double* out_reim) {
+  long np = 1;
+  while (np < n) np <<= 1;
+  cwt_ctx c = {wavelet, params, x, n, np, scales, ns, fs, padding, out_reim, NULL, NULL, 0};
+  fj_pool(B, 1, threads, cwt_signal_leaf, &c);
 }
 
 /* ------------------------------------------------------------------------ */

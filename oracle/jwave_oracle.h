@@ -106,9 +106,18 @@ void jwo_cwt_wavelet_t(int wavelet, const double* params, double t, double* re, 
 int jwo_cwt_direct(int wavelet, const double* params, const double* x, long n,
                    const double* scales, int ns, double fs, double* out);
 
-/* ---- batched wrappers for the CPU baseline (ForkJoin-equivalent, OpenMP over signals) ---- */
+/* ---- CPU baselines: the reference's ForkJoin patterns (OpenMP tasks, recursive halving) ---- */
 void jwo_modwt_fwdinv_batch(const double* x, long N, int J, const double* g, const double* h,
                             int L, int B, int use_fft, int threads, double* coeffs, double* xr);
+/* ParallelTransform 2-D forward (rows task, then columns task) + reverse (columns, rows) */
+void jwo_fwt2d_fwdrev_parallel(const double* x, int B, int rows, int cols, int lvlM, int lvlN,
+                               const double* sD, const double* wD, const double* sR,
+                               const double* wR, int M, int tw, int kind, int threads,
+                               double* y, double* xr);
+/* transformFFTParallel per signal, signals in the outer pool */
+void jwo_cwt_fft_parallel_batch(int wavelet, const double* params, const double* x, long n,
+                                const double* scales, int ns, double fs, int padding, int B,
+                                int threads, double* out_reim);
 
 #ifdef __cplusplus
 }

@@ -222,8 +222,36 @@ def cwt_fft(x, scales, fs=1.0, wavelet="morlet", params=(1.0, 1.0), padding=1, e
     return out[..., 0] + 1j * out[..., 1]
 
 
+def fwt2d_fwdrev_parallel(x, lvlM, lvlN, wavelet, threads=0):
+    """CPU baseline (cfg4): ParallelTransform 2-D forward then reverse of every matrix of x
+    (B x rows x cols): rows task then columns task, leaves of <= 16 lines."""
+    x = _f64(x)
+    B, rows, cols = x.shape
+    y, xr = np.empty_like(x), np.empty_like(x)
+    f = [_f64(v) for v in (wavelet.getScalingDeComposition(), wavelet.getWaveletDeComposition(),
+                           wavelet.getScalingReConstruction(), wavelet.getWaveletReConstruction())]
+    lib().jwo_fwt2d_fwdrev_parallel(_p(x), B, rows, cols, lvlM, lvlN, *[_p(v) for v in f],
+                                    f[0].shape[0], wavelet.getTransformWavelength(),
+                                    getattr(wavelet, "kind", 0), threads, _p(y), _p(xr))
+    return y, xr
+
+
+def cwt_fft_parallel_batch(x, scales, fs=1.0, wavelet="morlet", params=(1.0, 1.0), padding=1,
+                           threads=0):
+    """CPU baseline (cfg3): transformFFTParallel of every row of x (B x n), signals in the
+    outer pool, scales in parallel per signal; recurrence-twiddle FFT as the reference."""
+    x, sc = _f64(x), _f64(scales)
+    pr = _f64(list(params) + [0.0, 0.0])
+    B, n = x.shape
+    out = np.empty((B, sc.shape[0], n, 2))
+    lib().jwo_cwt_fft_parallel_batch(CWT_KINDS[wavelet] if isinstance(wavelet, str) else int(wavelet),
+                                     _p(pr), _p(x), ctypes.c_long(n), _p(sc), sc.shape[0],
+                                     ctypes.c_double(fs), padding, B, threads, _p(out))
+    return out[..., 0] + 1j * out[..., 1]
+
+
 def modwt_fwdinv_batch(x, J, g, h, use_fft=False, threads=0):
-    """CPU-baseline kernel: forward + inverse of every row of x, OpenMP over signals."""
+    """CPU-baseline kernel: forward + inverse of every row of x, ForkJoin halving over signals."""
     x, g, h = _f64(x), _f64(g), _f64(h)
     B, N = x.shape
     coeffs = np.empty((B, J + 1, N))

@@ -77,3 +77,67 @@ def test_two_rank_gloo_sharding_matches_single_process():
         assert total == n_items          # every signal processed exactly once
         assert maxerr < 1e-11        # db4 DIRECT recon of uniform input is ~2e-12
     assert [r[1] for r in res] == [0, 6] and [r[2] for r in res] == [6, 5]
+
+
+# ---------------------------------------------------------------- the bench's launcher
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run_ranks(world, args, local_ranks=None, timeout=240):
+    """Start `world` children of tests/_rank_worker.py (one process per rank, as
+    torch.distributed.run would) and return rank 0's JSON line."""
+    import json
+    import subprocess
+    import sys
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port),
+                   LOCAL_RANK=str(r if local_ranks is None else local_ranks[r]))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "_rank_worker.py")]
+                                      + args, env=env, stdout=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=timeout)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), [p.returncode for p in procs]
+    return json.loads([ln for ln in outs[0].splitlines() if ln.startswith("{")][-1])
+
+
+@pytest.mark.parametrize("gpus,extra,total", [(2, ["--global-batch", "8192", "--wavelet", "Symlet8",
+                                                   "--levels", "6"], 8192),
+                                              (4, [], 4096), (3, ["--global-batch", "1001"], 1001)])
+def test_bench_launcher_ranks_and_shards(gpus, extra, total):
+    # bench.py --gpus N (no torchrun): N rank processes with distinct RANK / LOCAL_RANK, one
+    # gloo group of N, and contiguous shards that cover the global batch exactly once
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus),
+                        "--launch-check"] + extra, env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = sorted((json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")),
+                   key=lambda d: d["rank"])
+    assert [d["rank"] for d in lines] == list(range(gpus))
+    assert [d["local_rank"] for d in lines] == list(range(gpus))
+    assert all(d["world"] == gpus and d["dist_world"] == gpus for d in lines)
+    assert all(d["global_batch"] == total for d in lines)
+    covered = []
+    for d in lines:
+        covered.extend(range(d["shard_start"], d["shard_start"] + d["shard_count"]))
+        assert d["seed_first"] == 42 + d["shard_start"]
+    assert covered == list(range(total))
+
+
+def test_rank_worker_oracle_shards_match_serial():
+    # the worker the GPU test drives, here on the oracle: 3 ranks, 11 signals
+    import oracle as orc
+    from jwave.transforms import wavelets as W
+    res = _run_ranks(3, ["--oracle", "--n", "512", "--levels", "5", "--items", "11"])
+    wv = W.Daubechies4()
+    g, h = orc.modwt_filters(wv.getScalingDeComposition(), wv.getWaveletDeComposition())
+    expect = [float(np.sum(orc.modwt_forward(orc.fill_uniform(512, 42 + i), 5, g, h, "direct_nz")))
+              for i in range(11)]
+    assert res["sums"] == expect
+    assert res["shards"] == [[0, 4], [4, 4], [8, 3]] and res["world"] == 3
+    assert res["recon"] < 1e-11

@@ -118,10 +118,62 @@ def test_fft_bluestein_tiny_lengths(n, J):
     assert np.max(np.abs(m.inverseMODWT(c) - x)) < 1e-10
 
 
-def test_auto_runs_direct_bit_exact():
+def _auto_fft(n, L, J, threshold=4096):
+    # MODWTTransform.performConvolution AUTO (:640-664), per level, int32 product
+    return any(orc.auto_uses_fft(n, (L - 1) * (1 << (j - 1)) + 1, threshold) for j in range(1, J + 1))
+
+
+@pytest.mark.parametrize("n,J,threshold", [(4096, 5, 4096), (64, 3, 4096), (512, 4, 4096),
+                                           (512, 1, 4096), (4096, 5, 2**31 - 1), (100, 3, 4096),
+                                           (1000, 3, 4096), (256, 3, -1)])
+def test_auto_follows_reference_rule(n, J, threshold):
+    # AUTO takes the FFT path exactly where the reference's N*M > fftConvolutionThreshold rule
+    # sends a convolution there (int32 product, :653); otherwise DIRECT, bit-exact
     wv = W.Daubechies4()
     g, h = ofilters(wv)
-    x = orc.fill_uniform(4096, 5)
-    m = MODWTTransform(wv)  # AUTO (the reference would pick FFT here: 4096*8 > 4096)
-    assert orc.auto_uses_fft(4096, 8)
-    assert bits_equal(m.forwardMODWT(x, 5), orc.modwt_forward(x, 5, g, h, "direct_nz"))
+    x = orc.fill_uniform(n, 5 + n)
+    auto = MODWTTransform(wv, fftThreshold=threshold)
+    c = auto.forwardMODWT(x, J)
+    xr = auto.inverseMODWT(c)
+    want_fft = _auto_fft(n, 8, J, threshold)
+    other = MODWTTransform(wv, fftThreshold=threshold)
+    other.setConvolutionMethod(ConvolutionMethod.FFT if want_fft else ConvolutionMethod.DIRECT)
+    assert bits_equal(c, other.forwardMODWT(x, J))
+    assert bits_equal(xr, other.inverseMODWT(c))
+    if not want_fft:
+        assert bits_equal(c, orc.modwt_forward(x, J, g, h, "direct_nz"))
+    rows_close(c, orc.modwt_forward(x, J, g, h, "direct_nz"))
+
+
+def test_auto_rule_int32_wrap_at_full_size():
+    # N = 2^20: db4 levels 1..9 pass N*M > 4096, level 10's product wraps negative (DIRECT in
+    # the reference); sym8 wraps from level 9 -- the rule the device evaluates is the oracle's
+    assert _auto_fft(1 << 20, 8, 8)
+    assert not orc.auto_uses_fft(1 << 20, 7 * 512 + 1)
+    assert not _auto_fft(8, 2, 2)
+
+
+@pytest.mark.parametrize("wname,J", [("Daubechies4", 8), ("Symlet8", 6)])
+def test_fft_path_full_size(wname, J, device):
+    # cfg2 / cfg5 geometry (N = 2^20) through the FFT path: every row within 1e-10 of the exact
+    # DIRECT oracle, and within 1e-9 of the reference's recurrence-twiddle FFT path (whose own
+    # drift from the exact convolution is ~1.7e-10 normwise here)
+    import ctypes
+    import torch
+    from jwave import _native
+    wv = W.by_name(wname)
+    g, h = ofilters(wv)
+    B, n = 2, 1 << 20
+    x = torch.empty((B, n), dtype=torch.float64, device=device)
+    _native.check(_native.lib().jw_synth_uniform(ctypes.c_void_p(x.data_ptr()), n, B, 42, None))
+    m = MODWTTransform(wv)
+    m.setConvolutionMethod(ConvolutionMethod.FFT)
+    c = m.forwardMODWT(x, J)
+    xr = m.inverseMODWT(c)
+    torch.cuda.synchronize()
+    assert (xr - x).abs().max().item() < 1e-10
+    x1 = orc.fill_uniform(n, 43)
+    got = c[1].cpu().numpy()
+    rows_close(got, orc.modwt_forward(x1, J, g, h, "direct_nz"))
+    jw = orc.modwt_forward(x1, J, g, h, "fft")
+    assert np.max(np.abs(got - jw)) / np.max(np.abs(jw)) < 1e-9

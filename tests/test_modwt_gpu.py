@@ -20,6 +20,14 @@ pytestmark = pytest.mark.gpu
 FMA_TOL = 1e-10  # normwise, north_star "within 1e-10 relative for Daubechies"
 
 
+def direct(wv, **kw):
+    """MODWTTransform with setConvolutionMethod(DIRECT): the bit-exact class (the default AUTO
+    takes the FFT path wherever the reference's N*M > fftThreshold rule does)."""
+    m = MODWTTransform(wv, **kw)
+    m.setConvolutionMethod(MODWTTransform.ConvolutionMethod.DIRECT)
+    return m
+
+
 def ofilters(wv):
     return orc.modwt_filters(wv.getScalingDeComposition(), wv.getWaveletDeComposition())
 
@@ -50,7 +58,7 @@ def test_strict_bit_exact_vs_oracle(wname, n, J):
     g, h = ofilters(wv)
     x = orc.fill_uniform(n, 42 + n) * 3.0
     ref = orc.modwt_forward(x, J, g, h, "direct_nz")
-    m = MODWTTransform(wv)
+    m = direct(wv)
     got = m.forwardMODWT(x, J)
     assert bits_equal(got, ref), f"max diff {np.max(np.abs(got - ref))}"
     xr_ref = orc.modwt_inverse(ref, g, h, "direct_nz")
@@ -66,7 +74,7 @@ def test_generic_kernels_bit_exact(wname, n, J, monkeypatch):
     g, h = ofilters(wv)
     x = orc.fill_uniform(n, 5 + n)
     ref = orc.modwt_forward(x, J, g, h, "direct_nz")
-    m = MODWTTransform(wv)
+    m = direct(wv)
     fast = m.forwardMODWT(x, J)
     monkeypatch.setenv("JW_MODWT_KERNEL", "generic")
     gen = m.forwardMODWT(x, J)
@@ -92,8 +100,8 @@ def test_inverse_kernel_variants_bit_exact(wname, n, J, ring, top, monkeypatch):
     monkeypatch.setenv("JW_INV_RING", ring)
     monkeypatch.setenv("JW_INV_TOP", top)
     ref = orc.modwt_inverse(c, g, h, "direct_nz")
-    assert bits_equal(MODWTTransform(wv).inverseMODWT(c), ref)
-    xr = MODWTTransform(wv, arith="fma").inverseMODWT(c)
+    assert bits_equal(direct(wv).inverseMODWT(c), ref)
+    xr = direct(wv, arith="fma").inverseMODWT(c)
     assert normwise(xr, ref) < FMA_TOL
 
 
@@ -110,8 +118,8 @@ def test_inverse_chunk_variants_bit_exact(wname, n, J, chunk, monkeypatch):
     monkeypatch.setenv("JW_INV_TOP", "global")
     monkeypatch.setenv("JW_INV_C", chunk)
     ref = orc.modwt_inverse(c, g, h, "direct_nz")
-    assert bits_equal(MODWTTransform(wv).inverseMODWT(c), ref)
-    xr = MODWTTransform(wv, arith="fma").inverseMODWT(c)
+    assert bits_equal(direct(wv).inverseMODWT(c), ref)
+    xr = direct(wv, arith="fma").inverseMODWT(c)
     assert normwise(xr, ref) < FMA_TOL
 
 
@@ -123,7 +131,7 @@ def test_strict_bit_exact_vs_faithful_oracle(wname, n, J):
     g, h = ofilters(wv)
     x = clean_signal(n)
     ref = orc.modwt_forward(x, J, g, h, "direct")
-    m = MODWTTransform(wv)
+    m = direct(wv)
     got = m.forwardMODWT(x, J)
     assert bits_equal(got, ref)
     assert bits_equal(m.inverseMODWT(got), orc.modwt_inverse(ref, g, h, "direct"))
@@ -136,7 +144,7 @@ def test_fma_within_tolerance(wname, n, J):
     g, h = ofilters(wv)
     x = orc.fill_uniform(n, 7)
     ref = orc.modwt_forward(x, J, g, h, "direct_nz")
-    m = MODWTTransform(wv, arith="fma")
+    m = direct(wv, arith="fma")
     got = m.forwardMODWT(x, J)
     for r in range(J + 1):
         assert normwise(got[r], ref[r]) < FMA_TOL
@@ -154,7 +162,7 @@ def test_batch_and_device_tensors(device):
     g, h = ofilters(wv)
     B, n, J = 5, 3000, 8
     x = np.stack([orc.fill_uniform(n, 100 + b) for b in range(B)])
-    m = MODWTTransform(wv)
+    m = direct(wv)
     host = m.forwardMODWT(x, J)
     assert host.shape == (B, J + 1, n)
     dev = m.forwardMODWT(torch.from_numpy(x).to(device), J)
@@ -190,7 +198,7 @@ def test_full_size_properties(device):
     B, n, J = 4, 1 << 20, 8
     x = torch.empty((B, n), dtype=torch.float64, device=device)
     _native.check(_native.lib().jw_synth_uniform(ctypes.c_void_p(x.data_ptr()), n, B, 42, None))
-    m = MODWTTransform(W.Daubechies4())
+    m = direct(W.Daubechies4())
     c = m.forwardMODWT(x, J)
     xr = m.inverseMODWT(c)
     torch.cuda.synchronize()
@@ -206,6 +214,35 @@ def test_full_size_properties(device):
     g, h = ofilters(W.Daubechies4())
     ref = orc.modwt_forward(orc.fill_uniform(n, 42 + 1), J, g, h, "direct_nz")
     assert bits_equal(c[1].cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("arith", ["strict", "fma"])
+def test_cfg5_geometry_full_size(arith, device):
+    # BASELINE configs[4] kernel: Symlet8, J = 6, N = 2^20 -- two signals against the oracle
+    # (STRICT bit for bit, FMA within 1e-10 normwise per row), reconstruction < 1e-11
+    import ctypes
+    import torch
+    from jwave import _native
+    wv = W.Symlet8()
+    g, h = ofilters(wv)
+    B, n, J = 2, 1 << 20, 6
+    x = torch.empty((B, n), dtype=torch.float64, device=device)
+    _native.check(_native.lib().jw_synth_uniform(ctypes.c_void_p(x.data_ptr()), n, B, 42, None))
+    m = direct(wv, arith=arith)
+    c = m.forwardMODWT(x, J)
+    xr = m.inverseMODWT(c)
+    torch.cuda.synchronize()
+    for b in range(B):
+        ref = orc.modwt_forward(orc.fill_uniform(n, 42 + b), J, g, h, "direct_nz")
+        got = c[b].cpu().numpy()
+        rec = orc.modwt_inverse(ref, g, h, "direct_nz")
+        if arith == "strict":
+            assert bits_equal(got, ref)
+            assert bits_equal(m.inverseMODWT(ref), rec)
+        else:
+            for r in range(J + 1):
+                assert normwise(got[r], ref[r]) < FMA_TOL
+    assert (xr - x).abs().max().item() < 1e-11
 
 
 def test_reconstruction_reference_cases():

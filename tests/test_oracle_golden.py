@@ -146,6 +146,27 @@ def test_haar_filters_vs_fixtures():
     assert np.max(np.abs(np.array(hw.getWaveletDeComposition()) - load_vector("filter_haar_dec_hi.txt"))) < 1e-10
 
 
+def test_daubechies_filters_vs_fixtures():
+    # testdata/filter_db2_dec_lo.txt ("Daubechies 2 = Haar", 2 taps) and filter_db4_dec_{lo,hi}.txt
+    # (4 taps) use the tap-count naming; JWave names by vanishing moments (DaubechiesK = 2K
+    # taps, Daubechies4.java:50-60), so they pin Haar1 and Daubechies2.  The high-pass fixture
+    # checks _buildOrthonormalSpace's alternating flip (Wavelet.java:104-122).  JWave's own
+    # decimal literals sit 3.4e-13 from the fixture's 17-digit values, inside the 1e-10 the
+    # reference's fixture tests use (CrossValidationTest.java:158-180).
+    assert np.array_equal(np.array(W.Haar1().getScalingDeComposition()),
+                          load_vector("filter_db2_dec_lo.txt"))
+    d2 = W.Daubechies2()
+    lo, hi = load_vector("filter_db4_dec_lo.txt"), load_vector("filter_db4_dec_hi.txt")
+    assert np.max(np.abs(np.array(d2.getScalingDeComposition()) - lo)) < 1e-12
+    assert np.max(np.abs(np.array(d2.getWaveletDeComposition()) - hi)) < 1e-12
+    # the flip itself is exact: wD[i] = (-1)^i sD[M-1-i]
+    sd = np.array(d2.getScalingDeComposition())
+    assert np.array_equal(np.array(d2.getWaveletDeComposition()), sd[::-1] * np.array([1, -1, 1, -1]))
+    # and the MODWT plan normalises these taps exactly as the oracle (MODWTTransform.java:599-606)
+    g, h = orc.modwt_filters(lo, hi)
+    assert abs(np.sum(g * g) - 0.5) < 1e-15 and abs(np.sum(h * h) - 0.5) < 1e-15
+
+
 def test_haar_level1_vs_fixtures():
     # transforms/CrossValidationTest.java:183-208 (fixtures are (a+-b)/sqrt2, 1 ulp off JWave)
     x = load_vector("haar_simple_input.txt")
