@@ -589,8 +589,18 @@ constexpr bool inv_fits_topg() {
 // thread of 256.  A/B variants (measured equal on MI355X): env
 // JW_INV_TOP=global reads level J's taps from global memory (TOPG: 43 KB of LDS, three
 // workgroups per CU for db4 J=8) and JW_INV_C=512 then takes two samples per thread.
+}  // namespace fast
+}  // namespace jw
+#include "jw_modwt_wave.hpp"
+namespace jw {
+namespace fast {
+
 template <int L, int J, bool FMA>
 int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hipStream_t s) {
+  if constexpr (wave::inv_wave_ok<L, J>()) {
+    const char* w = std::getenv("JW_INV_KERNEL");
+    if (w && w[0] == 'w') return wave::launch_inv_wave<L, J, FMA>(t, c, x, N, batch, s);
+  }
   constexpr int RF = J >= 7 ? 7 : J + 1;
   const char* e = std::getenv("JW_INV_RING");
   const char* top = std::getenv("JW_INV_TOP");

@@ -55,6 +55,8 @@ __global__ __launch_bounds__(NT) void inv_nomem(const double* __restrict__ coeff
 #pragma unroll
   for (int q = 0; q < D; ++q) fetch(S[q]);
   int rb[J + 1] = {};
+  double tv[R * 2 * L];
+  auto no_taps = [] {};
   __syncthreads();
   long a = N - C;
   for (long k = 0; k < steps / D; ++k) {
@@ -62,7 +64,8 @@ __global__ __launch_bounds__(NT) void inv_nomem(const double* __restrict__ coeff
     for (int q = 0; q < D; ++q) {
       // MEM 2: real x-hat stores (segment = whole row), else range-dropped
       const long P0 = MEM == 2 ? -(1L << 40) : (1L << 40);
-      inv_step<L, J, FMA, C, NT, RF>((d2*)lds, S[q], fetch, a, P0, 1L << 41, rx, taps, rb);
+      inv_step<L, J, FMA, C, NT, RF, false>((d2*)lds, S[q], fetch, a, P0, 1L << 41, rx, taps, rb, tv,
+                                            no_taps);
       a -= C;
       if (a < 0) a += N;
     }
