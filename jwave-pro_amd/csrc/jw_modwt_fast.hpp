@@ -598,8 +598,11 @@ namespace fast {
 template <int L, int J, bool FMA>
 int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hipStream_t s) {
   if constexpr (wave::inv_wave_ok<L, J>()) {
+    // the barrier-free kernel is the default wherever it fits; JW_INV_KERNEL=wg forces the
+    // workgroup kernel below (A/B runs and its parity tests)
     const char* w = std::getenv("JW_INV_KERNEL");
-    if (w && w[0] == 'w') return wave::launch_inv_wave<L, J, FMA>(t, c, x, N, batch, s);
+    if (!(w && w[0] == 'w' && w[1] == 'g'))
+      return wave::launch_inv_wave<L, J, FMA>(t, c, x, N, batch, s);
   }
   constexpr int RF = J >= 7 ? 7 : J + 1;
   const char* e = std::getenv("JW_INV_RING");

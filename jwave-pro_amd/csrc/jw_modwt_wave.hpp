@@ -32,7 +32,12 @@ constexpr int kW = 64;  // positions per step = lanes of the wave
 
 template <int L, int J>
 struct WGeo {
-  static constexpr int JL = J < 6 ? J : 6;  // LDS levels 1..JL (dilation <= 32)
+  static constexpr int JL = J < 5 ? J : 5;  // LDS levels 1..JL (dilation <= 16)
+  // level 6 (dilation 32): the tap at a + l + 32m is lane l's own pair (m even) or its partner
+  // lane l ^ 32's (m odd), so it lives in registers too: own pairs X[s-k] and partner pairs
+  // Z[s-k] = (l < 32 ? X_{l+32}[s-k] : X_{l-32}[s-k-1]), one permlane32 swap per word.
+  static constexpr bool P6 = J >= 6;
+  static constexpr int NX = L / 2 > 2 ? L / 2 : 2, NZ = L / 2;  // X[s-1] feeds the swap
   static constexpr int hist(int j) { return (L - 1) << (j - 1); }
   static constexpr int off(int j) {  // pair offset of LDS level j's [chunk | history]
     int o = 0;
@@ -45,7 +50,7 @@ struct WGeo {
   static constexpr int ring(int j) { return (L - 1) * q(j) + 1; }
   static constexpr int roff(int j) {  // offset of level j's shift register in the flat array
     int o = 0;
-    for (int i = JL + 1; i < j; ++i) o += ring(i);
+    for (int i = 7; i < j; ++i) o += ring(i);
     return o;
   }
   static constexpr int rtot = roff(J + 1) > 0 ? roff(J + 1) : 1;
@@ -59,6 +64,20 @@ struct WGeo {
   static constexpr int htot = hoff(JL + 1);
   static constexpr int H = (L - 1) * ((1 << J) - 1);
 };
+
+// Z = (lane < 32 ? cur of lane + 32 : prev of lane - 32): v_permlane32_swap exchanges lanes
+// 32..63 of its first operand with lanes 0..31 of its second.
+__device__ __forceinline__ d2 partner32(d2 cur, d2 prev, int lane) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 c = __builtin_bit_cast(u32x4, cur), p = __builtin_bit_cast(u32x4, prev);
+  u32x4 z;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const auto r = __builtin_amdgcn_permlane32_swap(c[w], p[w], false, false);
+    z[w] = lane < 32 ? r[1] : r[0];
+  }
+  return __builtin_bit_cast(d2, z);
+}
 
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -92,6 +111,9 @@ __global__ __launch_bounds__(kW) void modwt_inv_wave(const double* __restrict__ 
   d2 rg[G::rtot];
 #pragma unroll
   for (int i = 0; i < G::rtot; ++i) rg[i] = d2{0.0, 0.0};
+  d2 xr[G::NX], zr[G::NZ];  // level 6
+#pragma unroll
+  for (int i = 0; i < G::NX; ++i) xr[i] = zr[i] = d2{0.0, 0.0};
   d2 hp[G::htot > 0 ? G::htot : 1];
 #pragma unroll
   for (int i = 0; i < (G::htot > 0 ? G::htot : 1); ++i) hp[i] = d2{0.0, 0.0};
@@ -124,7 +146,7 @@ __global__ __launch_bounds__(kW) void modwt_inv_wave(const double* __restrict__ 
       double v = cur[J];  // V_J
       // register levels J .. JL+1
 #pragma unroll
-      for (int j = J; j > JL; --j) {
+      for (int j = J; j > 6; --j) {
         const int ro = G::roff(j), q = G::q(j);
 #pragma unroll
         for (int k = G::ring(j) - 1; k >= 1; --k) rg[ro + k] = rg[ro + k - 1];
@@ -136,6 +158,23 @@ __global__ __launch_bounds__(kW) void modwt_inv_wave(const double* __restrict__ 
           dp = madd<FMA>(dp, taps.b[m], rg[ro + m * q].y);
         }
         v = ap + dp;  // V_{j-1}
+      }
+      if constexpr (G::P6) {  // level 6: own / partner shift registers
+#pragma unroll
+        for (int k = G::NX - 1; k >= 1; --k) xr[k] = xr[k - 1];
+        xr[0] = d2{v, cur[5]};
+        const d2 z = partner32(xr[0], xr[1], lane);
+#pragma unroll
+        for (int k = G::NZ - 1; k >= 1; --k) zr[k] = zr[k - 1];
+        zr[0] = z;
+        double ap = 0.0, dp = 0.0;
+#pragma unroll
+        for (int m = 0; m < L; ++m) {
+          const d2 t = (m & 1) ? zr[m >> 1] : xr[m >> 1];
+          ap = madd<FMA>(ap, taps.a[m], t.x);
+          dp = madd<FMA>(dp, taps.b[m], t.y);
+        }
+        v = ap + dp;  // V_5
       }
       // LDS levels JL .. 1
 #pragma unroll
@@ -172,8 +211,9 @@ __global__ __launch_bounds__(kW) void modwt_inv_wave(const double* __restrict__ 
 
 template <int L, int J>
 constexpr bool inv_wave_ok() {
-  return L % 2 == 0 && J >= 7 && (size_t)WGeo<L, J>::lds_pairs * 16 <= 20 * 1024 &&
-         WGeo<L, J>::rtot <= 24;
+  using G = WGeo<L, J>;
+  return L % 2 == 0 && J >= 6 && (size_t)G::lds_pairs * 16 <= 20 * 1024 &&
+         (J >= 7 ? G::rtot : 0) + G::NX + G::NZ <= 31;
 }
 
 template <int L, int J, bool FMA>

@@ -97,6 +97,7 @@ def test_inverse_kernel_variants_bit_exact(wname, n, J, ring, top, monkeypatch):
     wv = W.by_name(wname)
     g, h = ofilters(wv)
     c = orc.modwt_forward(orc.fill_uniform(n, 11 + n), J, g, h, "direct_nz")
+    monkeypatch.setenv("JW_INV_KERNEL", "wg")  # these variants are the workgroup kernel's
     monkeypatch.setenv("JW_INV_RING", ring)
     monkeypatch.setenv("JW_INV_TOP", top)
     ref = orc.modwt_inverse(c, g, h, "direct_nz")
@@ -115,12 +116,42 @@ def test_inverse_chunk_variants_bit_exact(wname, n, J, chunk, monkeypatch):
     wv = W.by_name(wname)
     g, h = ofilters(wv)
     c = orc.modwt_forward(orc.fill_uniform(n, 13 + n), J, g, h, "direct_nz")
+    monkeypatch.setenv("JW_INV_KERNEL", "wg")
     monkeypatch.setenv("JW_INV_TOP", "global")
     monkeypatch.setenv("JW_INV_C", chunk)
     ref = orc.modwt_inverse(c, g, h, "direct_nz")
     assert bits_equal(direct(wv).inverseMODWT(c), ref)
     xr = direct(wv, arith="fma").inverseMODWT(c)
     assert normwise(xr, ref) < FMA_TOL
+
+
+WAVE_CASES = [  # shapes the barrier-free inverse (jw_modwt_wave.hpp) serves: J >= 6
+    ("Haar1", 512, 6), ("Haar1", 1000, 9), ("Haar1", 50000, 10), ("Daubechies2", 600, 9),
+    ("Daubechies2", 4097, 7), ("Daubechies3", 3001, 8), ("Daubechies4", 512, 8),
+    ("Daubechies4", 514, 7), ("Daubechies4", 70001, 8), ("Daubechies4", 4096, 6),
+    ("Daubechies4", 1 << 16, 8), ("Symlet8", 20000, 6), ("Symlet8", 4100, 6),
+    ("Daubechies6", 10001, 7), ("Coiflet2", 9000, 7),
+]
+
+
+@pytest.mark.parametrize("kernel", ["wave", "wg"])
+@pytest.mark.parametrize("wname,n,J", WAVE_CASES)
+def test_inverse_wave_vs_workgroup_bit_exact(wname, n, J, kernel, monkeypatch):
+    # one stream per wavefront (no barriers; dilation >= 32 levels in registers, permlane32
+    # swaps for dilation 32) against the workgroup-shared kernel: same bits in both contracts
+    wv = W.by_name(wname)
+    g, h = ofilters(wv)
+    c = orc.modwt_forward(orc.fill_uniform(n, 17 + n), J, g, h, "direct_nz")
+    monkeypatch.setenv("JW_INV_KERNEL", kernel)
+    ref = orc.modwt_inverse(c, g, h, "direct_nz")
+    assert bits_equal(direct(wv).inverseMODWT(c), ref)
+    xr = direct(wv, arith="fma").inverseMODWT(c)
+    assert normwise(xr, ref) < FMA_TOL
+    # batch of 3 with distinct rows: each wave's segment reads its own signal
+    cs = np.stack([c, c * 0.5, -c])
+    got = direct(wv).inverseMODWT(cs)
+    for b, k in enumerate([1.0, 0.5, -1.0]):
+        assert bits_equal(got[b], orc.modwt_inverse(c * k, g, h, "direct_nz"))
 
 
 @pytest.mark.parametrize("wname,n,J", [("Haar1", 64, 6), ("Daubechies4", 100, 5),

@@ -22,7 +22,23 @@ __global__ void clock_probe(unsigned long long* out) {
   if (acc == 12345.0) out[2] = 1;
 }
 
+__global__ void pl_check(unsigned* o) {
+  const int l = threadIdx.x;
+  const auto r = __builtin_amdgcn_permlane32_swap((unsigned)l, 100u + l, false, false);
+  o[l] = r[0];
+  o[64 + l] = r[1];
+}
+
 int main() {
+  {
+    unsigned* o;
+    hipMalloc(&o, 512);
+    pl_check<<<1, 64>>>(o);
+    unsigned h[128];
+    hipMemcpy(h, o, 512, hipMemcpyDeviceToHost);
+    printf("permlane32_swap(l, 100+l): r0[0]=%u r0[31]=%u r0[32]=%u r0[63]=%u | r1[0]=%u r1[31]=%u r1[32]=%u r1[63]=%u\n",
+           h[0], h[31], h[32], h[63], h[64], h[95], h[96], h[127]);
+  }
   const long N = 1L << 20;
   const int B = 1024;
   double *c, *x;
@@ -30,7 +46,7 @@ int main() {
   hipMalloc(&x, N * B * 8);
   hipMemset(c, 0, 9L * N * B * 8);
   Taps taps{};
-  for (int m = 0; m < 8; ++m) { taps.a[m] = 0.1 * m; taps.b[m] = 0.2 - 0.01 * m; }
+  for (int m = 0; m < 16; ++m) { taps.a[m] = 0.1 * m; taps.b[m] = 0.2 - 0.01 * m; }
   unsigned long long* ck;
   hipMalloc(&ck, 32);
   hipEvent_t e0, e1;
@@ -56,6 +72,8 @@ int main() {
   timeit("wave fma  (modwt_inv_wave)", [&] { wave::launch_inv_wave<8, 8, true>(taps, c, x, N, B, 0); });
   timeit("wg   strict", [&] { fast::launch_inv_c<8, 8, false, 256, 256, 2, 7>(taps, c, x, N, B, 0); });
   timeit("wave strict", [&] { wave::launch_inv_wave<8, 8, false>(taps, c, x, N, B, 0); });
+  timeit("wg   sym8 J6 fma", [&] { fast::launch_inv<16, 6, true>(taps, c, x, N, B, 0); });
+  timeit("wave sym8 J6 fma", [&] { wave::launch_inv_wave<16, 6, true>(taps, c, x, N, B, 0); });
   // compute only (wave kernel, MEM = 0) at the same grid
   {
     using G = wave::WGeo<8, 8>;
