@@ -97,6 +97,22 @@ def spawn_ranks(n):
     return max(rcs, key=abs)
 
 
+def inv_kernel_name(L, J, n):
+    """Which inverse MODWT kernel the library launches (csrc/jw_modwt_fast.hpp launch_inv and
+    jw_modwt_wave.hpp inv_wave_ok restated): the one-stream-per-wave kernel wherever it fits,
+    the workgroup-shared kernel otherwise or under JW_INV_KERNEL=wg."""
+    fast = L in (2, 4, 6, 8, 12, 16, 20) and J <= 10 and 512 <= n < (1 << 27)
+    if not fast:
+        return "modwt_inv_fused"
+    if os.environ.get("JW_INV_KERNEL", "").startswith("wg") or L % 2 or J < 6:
+        return "modwt_inv_fast"
+    hist = [(L - 1) << (j - 1) for j in range(1, J + 1)]
+    lds = sum(64 + hist[j - 1] for j in range(1, min(J, 5) + 1)) * 16
+    rtot = sum((L - 1) * (1 << (j - 7)) + 1 for j in range(7, J + 1))
+    ok = lds <= 20 * 1024 and rtot + max(L // 2, 2) + L // 2 <= 31
+    return "modwt_inv_wave" if ok else "modwt_inv_fast"
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -579,7 +595,9 @@ def main():
         # forward: read x (8 B) + write J+1 rows (8(J+1) B) per sample; inverse the mirror.
         bytes_per_sample = 8 * (1 + (J + 1))
         per_launch = bytes_per_sample * B * n
-        name, ms = ("modwt_inv_fast", inv_ms) if inv_ms >= fwd_ms else ("modwt_fwd_fast", fwd_ms)
+        L = len(wv.getScalingDeComposition())
+        name, ms = ((inv_kernel_name(L, J, n), inv_ms) if inv_ms >= fwd_ms
+                    else ("modwt_fwd_fast", fwd_ms))
         achieved = per_launch / (ms * 1e-3) / 1e9
         traffic = None
         if os.path.exists(TRAFFIC_FILE):

@@ -110,12 +110,13 @@ struct GeoF {
 __device__ __forceinline__ d2 bload2(rsrc_t r, int off) {
   return __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
+template <int CP = 0>
 __device__ __forceinline__ void bstore2(rsrc_t r, int off, d2 v) {
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, CP);
 }
 
-template <int L, int J, bool FMA, int NT, class Fetch>
+template <int L, int J, bool FMA, int NT, int SCP, class Fetch>
 __device__ __forceinline__ void fwd_step(double* lds, d2& cur, Fetch&& fetch, long a, long P,
                                          long seg_end, const rsrc_t (&rw)[J + 1],
                                          const Taps& taps) {
@@ -157,11 +158,11 @@ __device__ __forceinline__ void fwd_step(double* lds, d2& cur, Fetch&& fetch, lo
         v1 = madd<FMA>(v1, taps.a[m], pr.y);
       }
     }
-    bstore2(rw[j - 1], off, d2{w0, w1});
+    bstore2<SCP>(rw[j - 1], off, d2{w0, w1});
     if (j < J) {
       *(d2*)&lds[G::cs(j + 1) + i] = d2{v0, v1};
     } else {
-      bstore2(rw[J], off, d2{v0, v1});
+      bstore2<SCP>(rw[J], off, d2{v0, v1});
     }
     __syncthreads();
   }
@@ -184,7 +185,8 @@ __device__ __forceinline__ void fwd_step(double* lds, d2& cur, Fetch&& fetch, lo
   }
 }
 
-template <int L, int J, bool FMA, int NT>
+// SCP: cache-policy bits of the coefficient stores (A/B microbenchmarks; 0 in the product)
+template <int L, int J, bool FMA, int NT, int SCP = 0>
 __global__ __launch_bounds__(NT) void modwt_fwd_fast(const double* __restrict__ x,
                                                      double* __restrict__ coeffs, long N,
                                                      long seg_len, long warm, long npairs,
@@ -225,9 +227,9 @@ __global__ __launch_bounds__(NT) void modwt_fwd_fast(const double* __restrict__ 
   for (int k = 0; k < 2 * (J + 1); ++k) bstore(rx, kOOB - 8 * k, 0.0);  // distinct: not merged
   __syncthreads();
   for (long k = 0; k < npairs; ++k) {
-    fwd_step<L, J, FMA, NT>(lds, A, fetch, a, P, seg_end, rw, taps);
+    fwd_step<L, J, FMA, NT, SCP>(lds, A, fetch, a, P, seg_end, rw, taps);
     a += C;
-    fwd_step<L, J, FMA, NT>(lds, B, fetch, a, P, seg_end, rw, taps);
+    fwd_step<L, J, FMA, NT, SCP>(lds, B, fetch, a, P, seg_end, rw, taps);
     a += C;
   }
 }

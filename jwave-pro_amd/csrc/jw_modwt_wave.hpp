@@ -90,7 +90,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // index and shift-register slot is a compile-time register).
 // MEM = 0 (microbenchmarks only): the fetch makes register values and every store is dropped,
 // so the kernel times its LDS / VALU work alone.
-template <int L, int J, bool FMA, int D, int U, int MEM = 1>
+template <int L, int J, bool FMA, int D, int U, int MEM = 1, int CP = 0>
 __global__ __launch_bounds__(kW) void modwt_inv_wave(const double* __restrict__ coeffs,
                                                      double* __restrict__ x, long N, long seg_len,
                                                      long a_start, long ngroups, Taps taps) {
@@ -125,7 +125,9 @@ __global__ __launch_bounds__(kW) void modwt_inv_wave(const double* __restrict__ 
     p = p >= N ? p - N : p;
     const int off = (int)(p * 8);
 #pragma unroll
-    for (int j = 0; j <= J; ++j) dst[j] = MEM ? bload(rc[j], off) : (double)(p + j);
+    for (int j = 0; j <= J; ++j)
+      dst[j] = MEM ? __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rc[j], off, 0, CP))
+                   : (double)(p + j);
     lb -= kW;
     if (lb < 0) lb += N;
   };
