@@ -1,0 +1,133 @@
+package jwave.hip;
+
+import java.nio.ByteBuffer;
+import java.util.concurrent.atomic.AtomicInteger;
+
+import jwave.transforms.MODWTTransform;
+import jwave.transforms.wavelets.Wavelet;
+
+/**
+ * Drop-in for {@link MODWTTransform}: forwardMODWT / inverseMODWT run on the MI355X through
+ * jw_modwt_forward / jw_modwt_inverse (MODWTTransform.java:256-306, :337-375).  Callers keep
+ * {@code new Transform(new HipMODWTTransform(w))}; the flattened forward/reverse API (:388-443,
+ * :853-912) calls these overrides, so it needs no glue of its own.
+ *
+ * <p>DIRECT results are bit-identical to the JVM's with ARITH_STRICT (the default). AUTO keeps
+ * the reference's int32 rule (N * M_j > fftConvolutionThreshold takes the FFT path, :653).
+ * The plan (normalised filters, :452-484 and :599-606) is immutable and shared by all threads;
+ * {@link #clearFilterCache()} retires it once no call holds it.
+ */
+public class HipMODWTTransform extends MODWTTransform {
+  static {
+    HipEngine.load();
+  }
+
+  public static final int ARITH_STRICT = 0, ARITH_FMA = 1;
+
+  private final int arith;
+  private final Object planLock = new Object();
+  private Plan plan; // guarded by planLock
+
+  /** Reference-counted native plan: destroyed when retired and no call holds it. */
+  private static final class Plan {
+    final long handle;
+    final AtomicInteger users = new AtomicInteger(1); // 1 = the transform's own reference
+
+    Plan(long h) { handle = h; }
+
+    void release() {
+      if (users.decrementAndGet() == 0) nPlanDestroy(handle);
+    }
+  }
+
+  public HipMODWTTransform(Wavelet w) { this(w, ARITH_STRICT); }
+
+  public HipMODWTTransform(Wavelet w, int arith) {
+    super(w);
+    this.arith = arith;
+  }
+
+  public HipMODWTTransform(Wavelet w, int fftThreshold, int arith) {
+    super(w, fftThreshold); // MODWTTransform.java:191
+    this.arith = arith;
+  }
+
+  private Plan acquire() {
+    synchronized (planLock) {
+      if (plan == null) {
+        Wavelet w = getWavelet();
+        plan = new Plan(nPlanCreate(w.getScalingDeComposition(), w.getWaveletDeComposition(),
+                                    fftConvolutionThreshold, arith)); // protected field, :144
+      }
+      plan.users.incrementAndGet();
+      return plan;
+    }
+  }
+
+  @Override
+  public double[][] forwardMODWT(double[] data, int maxLevel) {
+    Plan p = acquire();
+    try {
+      return nForward(p.handle, data, maxLevel, getConvolutionMethod().ordinal());
+    } finally {
+      p.release();
+    }
+  }
+
+  @Override
+  public double[] inverseMODWT(double[][] coefficients) {
+    if (coefficients == null || coefficients.length == 0 || coefficients[0].length == 0)
+      return new double[0]; // MODWTTransform.java:338-346
+    Plan p = acquire();
+    try {
+      return nInverse(p.handle, coefficients, getConvolutionMethod().ordinal());
+    } finally {
+      p.release();
+    }
+  }
+
+  /**
+   * Batched forward over direct buffers (native order): x holds batch signals of n samples,
+   * coeffs receives batch x (maxLevel+1) x n.  One JNI crossing and one HBM staging for the
+   * whole batch.
+   */
+  public void forwardMODWT(ByteBuffer x, ByteBuffer coeffs, int n, int maxLevel, int batch) {
+    Plan p = acquire();
+    try {
+      nForwardDirect(p.handle, x, coeffs, n, maxLevel, batch, getConvolutionMethod().ordinal());
+    } finally {
+      p.release();
+    }
+  }
+
+  /** Batched inverse over direct buffers: coeffs batch x (levels+1) x n -> x batch x n. */
+  public void inverseMODWT(ByteBuffer coeffs, ByteBuffer x, int n, int levels, int batch) {
+    Plan p = acquire();
+    try {
+      nInverseDirect(p.handle, coeffs, x, n, levels, batch, getConvolutionMethod().ordinal());
+    } finally {
+      p.release();
+    }
+  }
+
+  @Override
+  public void clearFilterCache() {
+    super.clearFilterCache();
+    synchronized (planLock) {
+      if (plan != null) {
+        plan.release(); // freed now, or by the last in-flight call
+        plan = null;
+      }
+    }
+  }
+
+  private static native long nPlanCreate(double[] scalDec, double[] wavDec, int fftThreshold,
+                                         int arith);
+  private static native void nPlanDestroy(long plan);
+  private static native double[][] nForward(long plan, double[] x, int levels, int method);
+  private static native double[] nInverse(long plan, double[][] c, int method);
+  private static native void nForwardDirect(long plan, ByteBuffer x, ByteBuffer c, long n,
+                                            int levels, int batch, int method);
+  private static native void nInverseDirect(long plan, ByteBuffer c, ByteBuffer x, long n,
+                                            int levels, int batch, int method);
+}

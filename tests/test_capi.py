@@ -36,6 +36,23 @@ def test_library_exports_every_header_symbol():
     assert b"gfx950" in lib.jw_version()
 
 
+def test_jni_glue_binds_only_exported_symbols():
+    # jni/jwave_hip_jni.c (no JDK here to compile it): every engine call it makes is a declared,
+    # exported C-ABI symbol, and every native method of java/jwave/hip/ has its JNI function
+    src = open(os.path.join(ROOT, "jni", "jwave_hip_jni.c")).read()
+    src_nc = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    called = set(re.findall(r"\b(jw_[a-z0-9_]+)\s*\(", src_nc)) - {"jw_throw"}
+    assert called and called <= set(header_functions()), called - set(header_functions())
+    lib = _native.lib()
+    for name in called:
+        assert hasattr(lib, name), name
+    jdir = os.path.join(ROOT, "java", "jwave", "hip")
+    for f in sorted(os.listdir(jdir)):
+        cls = f[:-len(".java")]
+        for m in re.findall(r"\bnative\s+[\w\[\]]+\s+(n\w+)\s*\(", open(os.path.join(jdir, f)).read()):
+            assert f"Java_jwave_hip_{cls}_{m}(" in src, f"{cls}.{m} has no JNI function"
+
+
 @pytest.mark.parametrize("wname", W.ORTHONORMAL)
 def test_plan_filters_bit_identical_to_oracle(wname):
     # MODWTTransform.initializeFilterCache (:452-484) in the C-ABI plan vs the oracle

@@ -1,0 +1,17 @@
+"""The JW_HOST path driven from 8 C threads at once on one shared plan (tests/c/host_threads.c,
+MODWTThreadSafetyTest.java:23-104 pattern), every result bit-exact against the oracle."""
+import os
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+BIN = os.path.join(os.path.dirname(__file__), "c", "host_threads")
+
+
+def test_host_path_eight_threads_bit_exact():
+    assert os.path.exists(BIN), "tests/c/host_threads is built by __graft_entry__.build()"
+    r = subprocess.run([BIN], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 failures" in r.stdout
