@@ -269,14 +269,14 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   w.p2 = wavelet == JW_CWT_MORLET ? -2.0 * kPi * kPi * w.p0 : -0.5 * w.p0 * w.p0;
   JW_HIP_TRY(mem.alloc(&dsc, hsc.size() * sizeof(double)));
   JW_HIP_TRY(upload_async(dsc, hsc.data(), hsc.size() * sizeof(double), s));
-  int logN = 0;
-  while ((1L << logN) < N) ++logN;
-  const long N1 = N <= 4096 ? N : 1L << ((logN + 1) / 2);
+  // forward FFTs read the padded signals in natural order (split N1n); the spectra are stored
+  // column-major for the inverse FFTs' split N1 x N/N1 (fft::split_n1)
+  const long N1n = fft::split_n1(N, true), N1 = fft::split_n1(N, false);
   // forward FFT of the padded signals, gsig at a time
   for (long b0 = 0; b0 < batch && st == JW_OK; b0 += gsig) {
     const long nb = std::min<long>(gsig, batch - b0);
-    PadIn in{x + b0 * n, n, N <= 4096 ? 1 : N / N1, padding};
-    st = run_fft<-1>(N, nb, in, SpecOut1{X, N, b0}, SpecOut{X, N, N1, N / N1, b0}, A, s, T,
+    PadIn in{x + b0 * n, n, N / N1n, padding};
+    st = run_fft<-1>(N, nb, in, SpecOut1{X, N, b0}, SpecOut{X, N, N1n, N1, N / N1, b0}, A, s, T,
                      (ntm & 1) != 0);
   }
   // per (signal, scale) pair: IFFT(X * psi_hat) -> coefficients

@@ -1,6 +1,8 @@
 // jw_fft_passes.hpp -- the two FFT pass kernels and the four-step driver, shared by the
 // CWT (jw_cwt.hip) and MODWT FFT-convolution (jw_modwt_fft.hip) paths.  See jw_fft.hpp.
 #pragma once
+#include <type_traits>
+
 #include "jw_fft.hpp"
 
 namespace jw {
@@ -158,6 +160,91 @@ __global__ __launch_bounds__(256) void pass_generic(In in, Out out, long N, long
 }
 
 // ---------------------------------------------------------------------------------------
+// Long-line pass: one line of M = 512 R points (R = 2, 4, 8) per workgroup of R waves, the
+// line contiguous in memory on both sides.  Decimation in time over R: wave w takes the
+// subsequence x[R j + w] (j < 512) through fft512_wave, twiddles it by W_M^(w k), and the
+// workgroup finishes with R-point DFTs across the waves:
+//   X[k + 512 m] = sum_w W_R^(w m) (W_M^(w k) Y_w[k]),   k < 512, m < R.
+// The line is staged through LDS on the way in (coalesced global reads; the padded layout
+// makes the stride-R gathers bank-conflict free) and between the two stages.  TWID: times the
+// four-step twiddle W_N^(n line) of output n (pass 1).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int pad16(int j) { return j + (j >> 4); }
+__device__ __forceinline__ int pad8(int k) { return k + (k >> 3); }
+
+template <int S, int R>
+__device__ __forceinline__ void dftR(cplx (&v)[R]) {  // v[m] <- sum_w v[w] e^{S 2 pi i w m / R}
+  if constexpr (R == 2) {
+    const cplx a = v[0], b = v[1];
+    v[0] = cadd(a, b);
+    v[1] = csub(a, b);
+  } else if constexpr (R == 4) {
+    const cplx t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]);
+    const cplx t2 = cadd(v[1], v[3]), d = csub(v[1], v[3]);
+    const cplx t3 = make_double2(-S * d.y, S * d.x);  // d * e^{S i pi / 2}
+    v[0] = cadd(t0, t2);
+    v[2] = csub(t0, t2);
+    v[1] = cadd(t1, t3);
+    v[3] = csub(t1, t3);
+  } else {
+    static_assert(R == 8, "R = 2, 4 or 8");
+    dft8<S>(v);
+  }
+}
+
+template <int R>
+constexpr int big_lds() {  // complex entries: the padded line, or the R exchange buffers
+  return R * kXbuf > 512 * R + 32 * R ? R * kXbuf : 512 * R + 32 * R;
+}
+
+template <int S, int R, bool TWID, class In, class Out>
+__global__ __launch_bounds__(64 * R) void passbig(In in, Out out, long N, Tables T) {
+  constexpr int M = 512 * R, NT = 64 * R;
+  __shared__ cplx buf[big_lds<R>()];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const long item = blockIdx.y, line = blockIdx.x;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int j = tid + NT * i;
+    buf[pad16(j)] = in(item, j, line);
+  }
+  __syncthreads();
+  cplx a[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) a[r] = buf[pad16(R * (lane + 64 * r) + w)];
+  __syncthreads();  // buf becomes the waves' exchange buffers
+  fft512_wave<S>(a, buf + w * kXbuf, T.w512, lane);  // a[k2] = Y_w[q + 8 k1 + 64 k2]
+  const int q = lane >> 3, k1 = lane & 7;
+  const long step = N / M;  // W_M^x = W_N^(x N / M)
+  if (w > 0) {
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) {
+      const long k = q + 8 * k1 + 64 * k2;
+      a[k2] = cmul_tw<S>(a[k2], twiddle(T, w * k * step));
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k2 = 0; k2 < 8; ++k2) buf[w * kXbuf + pad8(q + 8 * k1 + 64 * k2)] = a[k2];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8 / R; ++i) {
+    const int k = tid + NT * i;
+    cplx v[R];
+#pragma unroll
+    for (int ww = 0; ww < R; ++ww) v[ww] = buf[ww * kXbuf + pad8(k)];
+    dftR<S, R>(v);
+#pragma unroll
+    for (int m = 0; m < R; ++m) {
+      const long n = k + 512 * m;
+      cplx o = v[m];
+      if (TWID) o = cmul_tw<S>(o, twiddle(T, (n * line) & (N - 1)));
+      out(item, n, line, o);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Shared functors
 // ---------------------------------------------------------------------------------------
 // Spectra are stored "column-major" for the inverse's four-step: element k at
@@ -182,12 +269,28 @@ struct ColOut {  // A[item][n1 * N2 + col]
     }
   }
 };
-struct SpecOut {  // X[item][k], k = n1 + N1 * n2, at its column-major position
+struct ColOutT {  // column-major workspace: A[item][col * N1 + n1] (long pass 1)
+  cplx* A;
+  long N, N1;
+  __device__ void operator()(long item, long n1, long col, cplx v) const {
+    A[item * N + col * N1 + n1] = v;
+  }
+};
+struct RowInT {  // row n1 of a column-major workspace: A[item][k2 * N1 + n1] (strided)
+  const cplx* A;
+  long N, N1;
+  __device__ cplx operator()(long item, long k2, long n1) const {
+    return A[item * N + k2 * N1 + n1];
+  }
+};
+// X[item][k], k = n1 + Nf * n2 (the forward FFT's output index, Nf its pass-1 length), stored
+// at its column-major position for the inverse's split (N1 x N2): contiguous pass-1 columns.
+struct SpecOut {
   cplx* X;
-  long N, N1, N2;
+  long N, Nf, N1, N2;
   long item0;
   __device__ void operator()(long item, long idx, long line, cplx v) const {
-    X[(item0 + item) * N + tpos(line + N1 * idx, N1, N2)] = v;
+    X[(item0 + item) * N + tpos(line + Nf * idx, N1, N2)] = v;
   }
 };
 struct SpecOut1 {  // single pass: X[item][idx]
@@ -203,11 +306,51 @@ struct SpecOut1 {  // single pass: X[item][idx]
 // result when N <= 4096 (one pass); otherwise pass 1 writes A and out_final receives
 // (item, n2, n1, v) for output index n1 + N1 n2.
 // One full FFT (forward or reverse) of `items` lines of length N: in(item, k) -> out.
+// Lengths 2^19 .. 2^21 split as 512 x M (M = 1024 .. 4096): the 512-point side runs pass512 (8
+// strided lines per workgroup), the long side passbig (one contiguous line per workgroup).
+// Which side goes first depends on the input: a natural-order (strided) input is read by
+// pass512 (N1 = 512, workspace row-major, pass 2 long rows); a column-major input (the
+// spectra, contiguous columns) by passbig (N1 = M, workspace column-major, pass 2 = pass512
+// over strided rows, so the natural-order output is written in 8-line pieces).
+inline bool long_split(long N) { return N >= (1L << 19) && N <= (1L << 21); }
+
+template <int S, class In1, class Out2>
+int run_fft_long(long N, long items, In1 in1, Out2 out_final, cplx* A, hipStream_t s,
+                 const Tables& T, bool a_nt) {
+  const long M = N / 512;
+  const int R = (int)(M / 512);
+  auto big = [&](auto rc, auto twid, auto in, auto out, long lines) {
+    constexpr int RR = decltype(rc)::value;
+    constexpr bool TW = decltype(twid)::value;
+    hipLaunchKernelGGL((passbig<S, RR, TW, decltype(in), decltype(out)>),
+                       dim3((unsigned)lines, (unsigned)items), dim3(64 * RR), 0, s, in, out, N, T);
+  };
+  auto big_r = [&](auto twid, auto in, auto out, long lines) {
+    if (R == 2) big(std::integral_constant<int, 2>{}, twid, in, out, lines);
+    else if (R == 4) big(std::integral_constant<int, 4>{}, twid, in, out, lines);
+    else big(std::integral_constant<int, 8>{}, twid, in, out, lines);
+  };
+  if constexpr (In1::kStrided) {  // N1 = 512, N2 = M
+    hipLaunchKernelGGL((pass512<S, true, true, In1, ColOut>), dim3((unsigned)(M / kT), (unsigned)items),
+                       dim3(512), 0, s, in1, ColOut{A, N, M, a_nt}, N, M, T);
+    JW_HIP_TRY(hipGetLastError());
+    big_r(std::false_type{}, RowIn{A, N, M}, out_final, 512L);
+  } else {  // N1 = M, N2 = 512
+    big_r(std::true_type{}, in1, ColOutT{A, N, M}, 512L);
+    JW_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL((pass512<S, true, false, RowInT, Out2>), dim3((unsigned)(M / kT), (unsigned)items),
+                       dim3(512), 0, s, RowInT{A, N, M}, out_final, N, 512L, T);
+  }
+  JW_HIP_TRY(hipGetLastError());
+  return JW_OK;
+}
+
 template <int S, class In1, class Out1, class Out2>
 int run_fft(long N, long items, In1 in1, Out1 out_single, Out2 out_final, cplx* A, hipStream_t s,
-            const Tables& T, bool a_nt) {
+            const Tables& T, bool a_nt, bool long_ok = true) {
   int logN = 0;
   while ((1L << logN) < N) ++logN;
+  if (long_ok && long_split(N)) return run_fft_long<S>(N, items, in1, out_final, A, s, T, a_nt);
   if (N <= 4096) {  // one pass, N2 = 1
     hipLaunchKernelGGL((pass_generic<S, true, In1, Out1>), dim3(1, (unsigned)items), dim3(256),
                        (size_t)N * sizeof(cplx), s, in1, out_single, N, 1L, logN, T);
@@ -277,12 +420,17 @@ int run_fft512_pipelined(long N, long items, long gsize, MkIn mk_in, MkOut mk_ou
 }
 
 // The four-step split used for length N: N1 = N (one pass) for N <= 4096, else
-// N1 = 2^ceil(log2 N / 2), N2 = N / N1.
+// N1 = 2^ceil(log2 N / 2), N2 = N / N1 (run_fft with long_ok = false).
 inline long split_n1(long N) {
   if (N <= 4096) return N;
   int logN = 0;
   while ((1L << logN) < N) ++logN;
   return 1L << ((logN + 1) / 2);
+}
+// The split run_fft takes for an input functor of the given kind (run_fft_long).
+inline long split_n1(long N, bool strided) {
+  if (long_split(N)) return strided ? 512 : N / 512;
+  return split_n1(N);
 }
 
 }  // namespace fft

@@ -23,22 +23,6 @@ namespace {
 using fft::cplx;
 using fft::Tables;
 
-// R[0][f] = G(f), R[1][f] = H(f), f < N
-__global__ void filter_response(cplx* R, Taps taps, int L, long N, Tables T) {
-  const long f = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= N) return;
-  cplx g = make_double2(0.0, 0.0), h = make_double2(0.0, 0.0);
-  for (int m = 0; m < L; ++m) {
-    const cplx w = fft::twiddle(T, (f * m) & (N - 1));  // e^{+2 pi i f m / N}; use conj
-    g.x += taps.a[m] * w.x;
-    g.y -= taps.a[m] * w.y;
-    h.x += taps.b[m] * w.x;
-    h.y -= taps.b[m] * w.y;
-  }
-  R[f] = g;
-  R[N + f] = h;
-}
-
 struct RealIn {  // row `item` of a real array, element k = N2 k1 + col (strided pass 1)
   static constexpr bool kStrided = true;
   const double* x;
@@ -57,68 +41,83 @@ struct RealOut {  // out row `item`: Re(v) / N at t = line + N1 idx
   }
 };
 
-// Forward: item = signal * (J+1) + row; row r < J is W_{r+1}, row J is V_J.
-struct FwdIn {
-  static constexpr bool kStrided = false;
-  const cplx* X;  // column-major spectra, one per signal
-  const cplx* R;
-  long N, N1, N2;
-  int J;
-  __device__ cplx operator()(long item, long k1, long col) const {
-    const long sig = item / (J + 1);
-    const int r = (int)(item - sig * (J + 1));
-    const long k = N2 * k1 + col;
-    // W_{r+1} = X H_{r+1} prod_{i<=r} G_i  (r < J);  V_J = X prod_{i<=J} G_i  (r = J)
-    const int ng = r < J ? r : J - 1;
-    cplx f = make_double2(1.0, 0.0);
-    for (int i = 1; i <= ng; ++i) f = fft::cmul(f, R[(k << (i - 1)) & (N - 1)]);  // G_i
-    f = fft::cmul(f, R[(r < J ? N : 0) + ((k << ng) & (N - 1))]);  // H_{r+1} or G_J
-    return fft::cmul(X[sig * N + col * N1 + k1], f);
+// The pyramid's per-row filter products, once per call (signal independent):
+//   F[r][k] = H_{r+1}(k) prod_{i<=r} G_i(k)  (r < J, row W_{r+1}),   F[J][k] = prod_{i<=J} G_i(k)
+// with G_i(k) = G(2^(i-1) k mod N), G(f) = sum_m g[m] z^m, z = e^{-2 pi i f/N} (exact table
+// twiddle for power-of-two N, sincospi of the reduced angle otherwise), by Horner's rule.
+// Stored at position t = pos(k) -- the spectra's own layout -- so the IFFT/FFT functors read
+// F with the same sequential index as the spectra (a response table indexed at the scaled
+// frequencies 2^(i-1) k would cost one cache line per element and level).
+__device__ __forceinline__ cplx fresp(const double* c, int L, cplx z) {
+  cplx v = make_double2(c[L - 1], 0.0);
+  for (int m = L - 2; m >= 0; --m) {
+    v = fft::cmul(v, z);
+    v.x += c[m];
   }
-};
+  return v;
+}
 
-// Inverse: item = signal; C = column-major spectra of the J+1 rows of every signal.
-struct InvIn {
-  static constexpr bool kStrided = false;
-  const cplx* C;
-  const cplx* R;
-  long N, N1, N2;
-  int J;
-  __device__ cplx operator()(long item, long k1, long col) const {
-    const long k = N2 * k1 + col, t = col * N1 + k1;
-    const cplx* c = C + item * (long)(J + 1) * N;
-    cplx s = c[(long)J * N + t];  // S_J = FFT(V_J)
-    for (int j = J; j >= 1; --j) {
-      const long f = (k << (j - 1)) & (N - 1);
-      const cplx g = R[f], h = R[N + f];
-      const cplx w = c[(long)(j - 1) * N + t];  // FFT(W_j)
-      s = make_double2(g.x * s.x + g.y * s.y + h.x * w.x + h.y * w.y,  // conj(G) S + conj(H) W
-                       g.x * s.y - g.y * s.x + h.x * w.y - h.y * w.x);
+template <bool POW2>
+__global__ void filter_products(cplx* __restrict__ F, Taps taps, int L, long N, int J, long N1,
+                                long N2, Tables T) {
+  const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= N) return;
+  const long t = POW2 ? fft::tpos(k, N1, N2) : k;
+  cplx p = make_double2(1.0, 0.0);
+  for (int i = 1; i <= J; ++i) {
+    cplx z;
+    if constexpr (POW2) {
+      const cplx w = fft::twiddle(T, (k << (i - 1)) & (N - 1));
+      z = make_double2(w.x, -w.y);
+    } else {
+      double sn, cs;
+      sincospi(2.0 * (double)(long)(((__int128)k << (i - 1)) % N) / (double)N, &sn, &cs);
+      z = make_double2(cs, -sn);
     }
-    return s;
+    F[(long)(i - 1) * N + t] = fft::cmul(p, fresp(taps.b, L, z));  // H_i prod_{<i} G
+    p = fft::cmul(p, fresp(taps.a, L, z));
   }
-};
+  F[(long)J * N + t] = p;
+}
 
-int prepare(long N, const ModwtPlan& p, Tables* T, cplx** R, StreamAllocs& mem, hipStream_t s) {
-  int st = fft::tables(N, T);
-  if (st != JW_OK) return st;
-  Taps taps;
+// Inverse adjoint sum S_0 = sum_r conj(F_r) C_r, C_r = FFT(row r) (the nested recursion
+// S_{j-1} = conj(G_j) S_j + conj(H_j) FFT(W_j) multiplied out).
+__device__ __forceinline__ cplx adjoint_sum(const cplx* c, const cplx* F, long N, int J, long t) {
+  cplx s = make_double2(0.0, 0.0);
+  for (int r = J; r >= 0; --r) {
+    const cplx f = F[(long)r * N + t], w = c[(long)r * N + t];
+    s.x += f.x * w.x + f.y * w.y;  // conj(f) w
+    s.y += f.x * w.y - f.y * w.x;
+  }
+  return s;
+}
+
+Taps taps_of(const ModwtPlan& p) {
+  Taps taps{};
   for (int m = 0; m < p.L; ++m) {
     taps.a[m] = p.g[m];
     taps.b[m] = p.h[m];
   }
-  JW_HIP_TRY(mem.alloc(R, (size_t)2 * N * sizeof(cplx)));
-  hipLaunchKernelGGL(filter_response, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, *R,
-                     taps, p.L, N, *T);
+  return taps;
+}
+
+// F: (J+1) x N filter products at the spectra's positions (power-of-two N: column-major
+// for the split N1 x N2; other N: natural order, N1 = N2 = 0)
+int products(const ModwtPlan& p, long N, int J, long N1, long N2, const Tables& T, cplx** F,
+             StreamAllocs& mem, hipStream_t s) {
+  JW_HIP_TRY(mem.alloc(F, (size_t)(J + 1) * N * sizeof(cplx)));
+  const unsigned nb = (unsigned)((N + 255) / 256);
+  if (N1 > 0) {
+    hipLaunchKernelGGL(filter_products<true>, dim3(nb), dim3(256), 0, s, *F, taps_of(p), p.L, N,
+                       J, N1, N2, T);
+  } else {
+    hipLaunchKernelGGL(filter_products<false>, dim3(nb), dim3(256), 0, s, *F, taps_of(p), p.L, N,
+                       J, 1L, 1L, T);
+  }
   JW_HIP_TRY(hipGetLastError());
   return JW_OK;
 }
 
-// signals per chunk so that the spectra + pass workspace stay near 1 GB
-long chunk_signals(long N, int J, int batch) {
-  const long per_sig = (long)(2 * (J + 1) + 1) * N * (long)sizeof(cplx);
-  return std::max(1L, std::min<long>(batch, (1L << 30) / per_sig));
-}
 
 // ---------------------------------------------------------------------------------------
 // Other lengths (FastFourierTransform.java:259-324 takes them through Bluestein): the same
@@ -162,6 +161,7 @@ __global__ void bs_pre(const cplx* __restrict__ in, cplx* __restrict__ a, const 
   const long item = i / M, m = i - item * M;
   a[i] = m < N ? fft::cmul(in[item * N + m], chirp(w, m, S)) : make_double2(0.0, 0.0);
 }
+// (elementwise, so any layout both spectra share: the column-major one of fft_to_spec)
 __global__ void bs_mul(cplx* __restrict__ a, const cplx* __restrict__ bh, long M, long items) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= items * M) return;
@@ -183,19 +183,36 @@ struct Bluestein {
   Tables T;
   cplx* w = nullptr;       // c_n, n < N
   cplx* bh[2] = {};        // FFT_M(b) for S = -1 (index 0) and S = +1 (index 1)
-  cplx* ws = nullptr;      // 2 x items x M workspace
+  cplx* ws = nullptr;      // 3 x items x M workspace: a, c and the inverse FFT's pass buffer
   long ws_items = 0;
 };  // device buffers owned by the caller's StreamAllocs
 
 unsigned blocks(long n) { return (unsigned)((n + 255) / 256); }
 
-int fft_natural(int S, long M, long items, const cplx* in, cplx* out, cplx* A, hipStream_t s,
+// Column-major spectra of length M (element k at tpos(k, N1c, N2c), the layout the inverse's
+// pass 1 reads as contiguous columns; natural order for M <= 4096).
+struct TposIn {
+  static constexpr bool kStrided = false;
+  const cplx* a;
+  long M, N1, N2;
+  __device__ cplx operator()(long item, long k1, long col) const {
+    return a[item * M + col * N1 + k1];
+  }
+};
+
+// FFT_M of natural-order rows -> column-major spectra
+int fft_to_spec(long M, long items, const cplx* in, cplx* out, cplx* A, hipStream_t s,
                 const Tables& T) {
-  const long N1 = fft::split_n1(M), N2 = M / N1;
-  return S < 0 ? fft::run_fft<-1>(M, items, NatIn{in, M, N2}, NatOut1{out, M}, NatOut{out, M, N1},
-                                  A, s, T, false)
-               : fft::run_fft<1>(M, items, NatIn{in, M, N2}, NatOut1{out, M}, NatOut{out, M, N1},
-                                 A, s, T, false);
+  const long N1n = fft::split_n1(M, true), N1c = fft::split_n1(M, false);
+  return fft::run_fft<-1>(M, items, NatIn{in, M, M / N1n}, NatOut1{out, M},
+                          fft::SpecOut{out, M, N1n, N1c, M / N1c, 0}, A, s, T, false);
+}
+// IFFT_M (no 1/M) of column-major spectra -> natural-order rows
+int ifft_from_spec(long M, long items, const cplx* in, cplx* out, cplx* A, hipStream_t s,
+                   const Tables& T) {
+  const long N1c = fft::split_n1(M, false);
+  return fft::run_fft<1>(M, items, TposIn{in, M, N1c, M / N1c}, NatOut1{out, M},
+                         NatOut{out, M, N1c}, A, s, T, false);
 }
 
 int bluestein_init(Bluestein* B, long N, long max_items, StreamAllocs& mem, hipStream_t s) {
@@ -216,7 +233,7 @@ int bluestein_init(Bluestein* B, long N, long max_items, StreamAllocs& mem, hipS
   JW_HIP_TRY(mem.alloc(&B->w, N * sizeof(cplx)));
   JW_HIP_TRY(mem.alloc(&B->bh[0], 2 * M * sizeof(cplx)));
   B->bh[1] = B->bh[0] + M;
-  JW_HIP_TRY(mem.alloc(&B->ws, (size_t)2 * max_items * M * sizeof(cplx)));
+  JW_HIP_TRY(mem.alloc(&B->ws, (size_t)3 * max_items * M * sizeof(cplx)));
   JW_HIP_TRY(upload_async(B->w, hw.data(), N * sizeof(cplx), s));
   // b_m for both signs, then their FFTs (two items of length M)
   std::vector<cplx> hb(2 * M, make_double2(0.0, 0.0));
@@ -230,7 +247,7 @@ int bluestein_init(Bluestein* B, long N, long max_items, StreamAllocs& mem, hipS
   cplx* tmp = B->ws;  // the workspace's first 2M entries stage b
   JW_HIP_TRY(upload_async(tmp, hb.data(), 2 * M * sizeof(cplx), s));
   // pass workspace: the next 2M entries (ws holds 2 x max_items x M, max_items = batch (J+1) >= 2)
-  return fft_natural(-1, M, 2, tmp, B->bh[0], B->ws + 2 * M, s, B->T);
+  return fft_to_spec(M, 2, tmp, B->bh[0], B->ws + 2 * M, s, B->T);  // column-major, as bs_mul
 }
 
 // items length-N DFTs (S = -1 forward, +1 reverse without 1/N), natural order in -> out
@@ -238,36 +255,20 @@ int bluestein_dft(const Bluestein& B, int S, long items, const cplx* in, cplx* o
   const long N = B.N, M = B.M;
   for (long i0 = 0; i0 < items; i0 += B.ws_items) {
     const long ni = std::min(B.ws_items, items - i0);
-    cplx *a = B.ws, *c = B.ws + ni * M;
+    // the inverse FFT reads column-major c and its pass 1 writes rows: its own workspace p
+    cplx *a = B.ws, *c = B.ws + ni * M, *p = B.ws + 2 * ni * M;
     hipLaunchKernelGGL(bs_pre, dim3(blocks(ni * M)), dim3(256), 0, s, in + i0 * N, a, B.w, N, M,
                        ni, S);
-    int st = fft_natural(-1, M, ni, a, c, a, s, B.T);  // FFT_M(a) -> c (a is the pass workspace)
+    int st = fft_to_spec(M, ni, a, c, a, s, B.T);  // FFT_M(a) -> c (a is the pass workspace)
     if (st != JW_OK) return st;
     hipLaunchKernelGGL(bs_mul, dim3(blocks(ni * M)), dim3(256), 0, s, c, B.bh[S < 0 ? 0 : 1], M, ni);
-    st = fft_natural(1, M, ni, c, a, c, s, B.T);  // IFFT_M (no 1/M) -> a
+    st = ifft_from_spec(M, ni, c, a, p, s, B.T);  // IFFT_M (no 1/M) -> a, natural order
     if (st != JW_OK) return st;
     hipLaunchKernelGGL(bs_post, dim3(blocks(ni * N)), dim3(256), 0, s, a, out + i0 * N, B.w, N, M,
                        ni, S);
     JW_HIP_TRY(hipGetLastError());
   }
   return JW_OK;
-}
-
-// R[0][f] = G(f), R[1][f] = H(f) for any N: e^{-2 pi i (f m mod N)/N}
-__global__ void filter_response_any(cplx* R, Taps taps, int L, long N) {
-  const long f = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= N) return;
-  cplx g = make_double2(0.0, 0.0), h = make_double2(0.0, 0.0);
-  for (int m = 0; m < L; ++m) {
-    double sn, cs;
-    sincospi(2.0 * (double)((f * m) % N) / (double)N, &sn, &cs);
-    g.x += taps.a[m] * cs;
-    g.y -= taps.a[m] * sn;
-    h.x += taps.b[m] * cs;
-    h.y -= taps.b[m] * sn;
-  }
-  R[f] = g;
-  R[N + f] = h;
 }
 
 __global__ void real_to_cplx(const double* __restrict__ x, cplx* __restrict__ y, long n) {
@@ -280,59 +281,34 @@ __global__ void cplx_re_scaled(const cplx* __restrict__ y, double* __restrict__ 
   if (i < n) x[i] = y[i].x * inv;
 }
 // forward pyramid in frequency, natural order: Y[sig][r][k] = X[sig][k] F_r(k)
-__global__ void fwd_combine(const cplx* __restrict__ X, const cplx* __restrict__ R,
+__global__ void fwd_combine(const cplx* __restrict__ X, const cplx* __restrict__ F,
                             cplx* __restrict__ Y, long N, int J, long nsig) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nsig * (J + 1) * N) return;
   const long k = i % N, item = i / N, sig = item / (J + 1);
-  const int r = (int)(item - sig * (J + 1));
-  const int ng = r < J ? r : J - 1;
-  cplx f = make_double2(1.0, 0.0);
-  for (int q = 1; q <= ng; ++q) f = fft::cmul(f, R[(long)(((__int128)k << (q - 1)) % N)]);
-  f = fft::cmul(f, R[(r < J ? N : 0) + (long)(((__int128)k << ng) % N)]);
-  Y[i] = fft::cmul(X[sig * N + k], f);
+  const long r = item - sig * (J + 1);
+  Y[i] = fft::cmul(X[sig * N + k], F[r * N + k]);
 }
-// inverse: S[sig][k] from C[sig][r][k] = FFT(row r)
-__global__ void inv_combine(const cplx* __restrict__ C, const cplx* __restrict__ R,
+// inverse: S[sig][k] = sum_r conj(F_r(k)) C[sig][r][k], C[sig][r] = FFT(row r)
+__global__ void inv_combine(const cplx* __restrict__ C, const cplx* __restrict__ F,
                             cplx* __restrict__ Sout, long N, int J, long nsig) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nsig * N) return;
   const long sig = i / N, k = i - sig * N;
-  const cplx* c = C + sig * (long)(J + 1) * N;
-  cplx sv = c[(long)J * N + k];
-  for (int j = J; j >= 1; --j) {
-    const long f = (long)(((__int128)k << (j - 1)) % N);
-    const cplx g = R[f], h = R[N + f];
-    const cplx w = c[(long)(j - 1) * N + k];
-    sv = make_double2(g.x * sv.x + g.y * sv.y + h.x * w.x + h.y * w.y,
-                      g.x * sv.y - g.y * sv.x + h.x * w.y - h.y * w.x);
-  }
-  Sout[i] = sv;
-}
-
-int prepare_any(long N, const ModwtPlan& p, cplx** R, StreamAllocs& mem, hipStream_t s) {
-  Taps taps;
-  for (int m = 0; m < p.L; ++m) {
-    taps.a[m] = p.g[m];
-    taps.b[m] = p.h[m];
-  }
-  JW_HIP_TRY(mem.alloc(R, (size_t)2 * N * sizeof(cplx)));
-  hipLaunchKernelGGL(filter_response_any, dim3(blocks(N)), dim3(256), 0, s, *R, taps, p.L, N);
-  JW_HIP_TRY(hipGetLastError());
-  return JW_OK;
+  Sout[i] = adjoint_sum(C + sig * (long)(J + 1) * N, F, N, J, k);
 }
 
 // per-chunk signals for the general path: rows, spectra and the chirp workspace ~1 GB
 long chunk_any(long N, long M, int J, int batch) {
-  const long per_sig = ((long)(J + 1) * (2 * N + 2 * M) + 2 * N) * (long)sizeof(cplx);
+  const long per_sig = ((long)(J + 1) * (2 * N + 3 * M) + 2 * N) * (long)sizeof(cplx);
   return std::max(1L, std::min<long>(batch, (1L << 30) / per_sig));
 }
 
 int forward_any(const ModwtPlan& p, const double* x, double* coeffs, long N, int J, int batch,
                 hipStream_t s) {
   StreamAllocs mem(s);
-  cplx* R = nullptr;
-  int st = prepare_any(N, p, &R, mem, s);
+  cplx* R = nullptr;  // filter products, natural order
+  int st = products(p, N, J, 0, 0, Tables{}, &R, mem, s);
   if (st != JW_OK) return st;
   long M = 1;
   while (M < 2 * N - 1) M <<= 1;
@@ -361,8 +337,8 @@ int forward_any(const ModwtPlan& p, const double* x, double* coeffs, long N, int
 int inverse_any(const ModwtPlan& p, const double* coeffs, double* x, long N, int J, int batch,
                 hipStream_t s) {
   StreamAllocs mem(s);
-  cplx* R = nullptr;
-  int st = prepare_any(N, p, &R, mem, s);
+  cplx* R = nullptr;  // filter products, natural order
+  int st = products(p, N, J, 0, 0, Tables{}, &R, mem, s);
   if (st != JW_OK) return st;
   long M = 1;
   while (M < 2 * N - 1) M <<= 1;
@@ -440,8 +416,9 @@ int fft_device(int S, const double* in, double* out, long n, long batch, hipStre
       const NatIn fin{x + b0 * n, n, N2};
       const NatOut1S o1{y + b0 * n, n, scale};
       const NatOutS o2{y + b0 * n, n, N1, scale};
-      st = S < 0 ? fft::run_fft<-1>(n, nb, fin, o1, o2, A, s, T, false)
-                 : fft::run_fft<1>(n, nb, fin, o1, o2, A, s, T, false);
+      // natural order in and out: the legacy split (long_ok = false)
+      st = S < 0 ? fft::run_fft<-1>(n, nb, fin, o1, o2, A, s, T, false, false)
+                 : fft::run_fft<1>(n, nb, fin, o1, o2, A, s, T, false, false);
     }
     return st;
   }
@@ -449,7 +426,7 @@ int fft_device(int S, const double* in, double* out, long n, long batch, hipStre
   if (n > (1L << 23)) return fail(JW_ERR_UNSUPPORTED, "FFT length %ld > 2^23 (not a power of 2)", n);
   long M = 1;
   while (M < 2 * n - 1) M <<= 1;
-  const long items = std::max(2L, std::min<long>(batch, (1L << 30) / (2 * M * (long)sizeof(cplx))));
+  const long items = std::max(2L, std::min<long>(batch, (1L << 30) / (3 * M * (long)sizeof(cplx))));
   Bluestein B;
   int st = bluestein_init(&B, n, items, mem, s);
   if (st != JW_OK) return st;
@@ -467,28 +444,135 @@ static bool is_pow2(long N) { return (N & (N - 1)) == 0; }
 // power-of-two N: the four-step pyramid; other N (< 2^23): the chirp-z pyramid
 bool modwt_fft_supported(long N) { return N >= 2 && N <= (1L << 23); }
 
+namespace {
+// ---------------------------------------------------------------------------------------
+// Power-of-two N: two real rows per complex transform.  Every spectrum of the pyramid is
+// Hermitian (real signals, real filters), so rows a = 2q and b = 2q+1 share one complex FFT:
+//   forward:  W_a + i W_b = IFFT(X (F_a + i F_b))                 (P1_q = F_a + i F_b)
+//   inverse:  Z_q = FFT(row_a + i row_b),  FFT(row_a) = (Z_q[k] + conj Z_q[-k]) / 2,
+//             FFT(row_b) = (Z_q[k] - conj Z_q[-k]) / 2i, so the adjoint sum is
+//             S_0[k] = 1/2 sum_q conj(P1_q[k]) Z_q[k] + conj(P2_q[k]) conj(Z_q[-k])
+//                                                                  (P2_q = F_a - i F_b)
+// An odd last row pairs with zero (F_b = 0).  Half the transforms of the row-by-row pyramid;
+// the same values up to rounding (the FFT path's tolerance class, 1e-10 of DIRECT).
+// ---------------------------------------------------------------------------------------
+__global__ void pair_products(cplx* __restrict__ P, const cplx* __restrict__ F, long N, int J) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N) return;
+  const int Q = (J + 2) / 2;
+  for (int q = 0; q < Q; ++q) {
+    const cplx fa = F[(long)(2 * q) * N + t];
+    const cplx fb = 2 * q + 1 <= J ? F[(long)(2 * q + 1) * N + t] : make_double2(0.0, 0.0);
+    P[(long)q * N + t] = make_double2(fa.x - fb.y, fa.y + fb.x);             // F_a + i F_b
+    P[(long)(Q + q) * N + t] = make_double2(fa.x + fb.y, fa.y - fb.x);       // F_a - i F_b
+  }
+}
+
+struct FwdIn2 {  // item = signal * Q + q: X * P1_q
+  static constexpr bool kStrided = false;
+  const cplx* X;
+  const cplx* P;
+  long N, N1, N2;
+  int Q;
+  __device__ cplx operator()(long item, long k1, long col) const {
+    const long sig = item / Q, q = item - sig * Q, t = col * N1 + k1;
+    return fft::cmul(X[sig * N + t], P[q * N + t]);
+  }
+};
+struct RealOut2 {  // rows 2q <- Re v / N, 2q+1 <- Im v / N (if it exists), t = line + N1 idx
+  double* out;
+  long N, N1;
+  int J, Q;
+  double inv_n;
+  __device__ void operator()(long item, long idx, long line, cplx v) const {
+    const long sig = item / Q, q = item - sig * Q, t = line + N1 * idx;
+    double* o = out + (sig * (J + 1) + 2 * q) * N + t;
+    o[0] = v.x * inv_n;
+    if (2 * q + 1 <= J) o[N] = v.y * inv_n;
+  }
+};
+struct RealIn2 {  // item = signal * Q + q: row 2q + i row 2q+1, element k = N2 k1 + col
+  static constexpr bool kStrided = true;
+  const double* x;
+  long N, N2;
+  int J, Q;
+  __device__ cplx operator()(long item, long k1, long col) const {
+    const long sig = item / Q, q = item - sig * Q, k = N2 * k1 + col;
+    const double* r = x + (sig * (J + 1) + 2 * q) * N + k;
+    return make_double2(r[0], 2 * q + 1 <= J ? r[N] : 0.0);
+  }
+};
+struct InvIn2 {  // item = signal; Z: Q column-major spectra per signal
+  static constexpr bool kStrided = false;
+  const cplx* Z;
+  const cplx* P;
+  long N, N1, N2;
+  int Q;
+  __device__ cplx operator()(long item, long k1, long col) const {
+    const long k = N2 * k1 + col, t = col * N1 + k1;
+    const long km = (N - k) & (N - 1), tm = fft::tpos(km, N1, N2);
+    const cplx* z = Z + item * (long)Q * N;
+    cplx s = make_double2(0.0, 0.0);
+    for (int q = Q - 1; q >= 0; --q) {
+      const cplx p1 = P[(long)q * N + t], p2 = P[(long)(Q + q) * N + t];
+      const cplx zk = z[(long)q * N + t], zm = z[(long)q * N + tm];
+      // conj(p1) zk + conj(p2) conj(zm)
+      s.x += p1.x * zk.x + p1.y * zk.y + p2.x * zm.x - p2.y * zm.y;
+      s.y += p1.x * zk.y - p1.y * zk.x - p2.x * zm.y - p2.y * zm.x;
+    }
+    return make_double2(0.5 * s.x, 0.5 * s.y);
+  }
+};
+
+// filter products F ((J+1) rows, scratch) -> pair tables P (2Q rows), spectra layout
+int pair_tables(const ModwtPlan& p, long N, int J, long N1, long N2, const Tables& T, cplx** P,
+                StreamAllocs& mem, hipStream_t s) {
+  cplx* F = nullptr;
+  int st = products(p, N, J, N1, N2, T, &F, mem, s);
+  if (st != JW_OK) return st;
+  const int Q = (J + 2) / 2;
+  JW_HIP_TRY(mem.alloc(P, (size_t)2 * Q * N * sizeof(cplx)));
+  hipLaunchKernelGGL(pair_products, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, *P, F, N, J);
+  JW_HIP_TRY(hipGetLastError());
+  return JW_OK;
+}
+
+// signals per chunk: spectra + pass workspace of about 4 GB (HBM holds 288 GB; bigger chunks
+// mean fewer, fuller launches)
+long chunk_pairs(long N, int J, int batch) {
+  const int Q = (J + 2) / 2;
+  const long per_sig = (long)(2 * Q + 1) * N * (long)sizeof(cplx);
+  return std::max(1L, std::min<long>(batch, (4L << 30) / per_sig));
+}
+}  // namespace
+
 int modwt_forward_fft_device(const ModwtPlan& p, const double* x, double* coeffs, long N, int J,
                              int batch, hipStream_t s) {
   if (!is_pow2(N)) return forward_any(p, x, coeffs, N, J, batch, s);
   StreamAllocs mem(s);
   Tables T;
-  cplx* R = nullptr;
-  int st = prepare(N, p, &T, &R, mem, s);
+  int st = fft::tables(N, &T);
   if (st != JW_OK) return st;
-  const long N1 = fft::split_n1(N), N2 = N / N1;
-  const long bc = chunk_signals(N, J, batch);
+  // forward FFTs read natural-order rows (split N1n), the inverse FFTs column-major spectra
+  // (split N1 x N2, the spectra's layout)
+  const long N1n = fft::split_n1(N, true), N1 = fft::split_n1(N, false), N2 = N / N1;
+  const int Q = (J + 2) / 2;
+  cplx* P = nullptr;
+  st = pair_tables(p, N, J, N1, N2, T, &P, mem, s);
+  if (st != JW_OK) return st;
+  const long bc = chunk_pairs(N, J, batch);
   cplx *X = nullptr, *A = nullptr;
   JW_HIP_TRY(mem.alloc(&X, (size_t)bc * N * sizeof(cplx)));
-  JW_HIP_TRY(mem.alloc(&A, (size_t)bc * (J + 1) * N * sizeof(cplx)));
+  JW_HIP_TRY(mem.alloc(&A, (size_t)bc * Q * N * sizeof(cplx)));
   for (long b0 = 0; b0 < batch && st == JW_OK; b0 += bc) {
     const long nb = std::min<long>(bc, batch - b0);
-    st = fft::run_fft<-1>(N, nb, RealIn{x + b0 * N, N, N2}, fft::SpecOut1{X, N, 0},
-                          fft::SpecOut{X, N, N1, N2, 0}, A, s, T, false);
+    st = fft::run_fft<-1>(N, nb, RealIn{x + b0 * N, N, N / N1n}, fft::SpecOut1{X, N, 0},
+                          fft::SpecOut{X, N, N1n, N1, N2, 0}, A, s, T, false);
     if (st != JW_OK) break;
     const double inv = 1.0 / (double)N;
     double* o = coeffs + b0 * (long)(J + 1) * N;
-    st = fft::run_fft<1>(N, nb * (J + 1), FwdIn{X, R, N, N1, N2, J}, RealOut{o, N, 1, inv},
-                         RealOut{o, N, N1, inv}, A, s, T, false);
+    st = fft::run_fft<1>(N, nb * Q, FwdIn2{X, P, N, N1, N2, Q}, RealOut2{o, N, 1, J, Q, inv},
+                         RealOut2{o, N, N1, J, Q, inv}, A, s, T, false);
   }
   return st;
 }
@@ -498,21 +582,25 @@ int modwt_inverse_fft_device(const ModwtPlan& p, const double* coeffs, double* x
   if (!is_pow2(N)) return inverse_any(p, coeffs, x, N, J, batch, s);
   StreamAllocs mem(s);
   Tables T;
-  cplx* R = nullptr;
-  int st = prepare(N, p, &T, &R, mem, s);
+  int st = fft::tables(N, &T);
   if (st != JW_OK) return st;
-  const long N1 = fft::split_n1(N), N2 = N / N1;
-  const long bc = chunk_signals(N, J, batch);
-  cplx *C = nullptr, *A = nullptr;
-  JW_HIP_TRY(mem.alloc(&C, (size_t)bc * (J + 1) * N * sizeof(cplx)));
-  JW_HIP_TRY(mem.alloc(&A, (size_t)bc * (J + 1) * N * sizeof(cplx)));
+  const long N1n = fft::split_n1(N, true), N1 = fft::split_n1(N, false), N2 = N / N1;
+  const int Q = (J + 2) / 2;
+  cplx* P = nullptr;
+  st = pair_tables(p, N, J, N1, N2, T, &P, mem, s);
+  if (st != JW_OK) return st;
+  const long bc = chunk_pairs(N, J, batch);
+  cplx *Z = nullptr, *A = nullptr;
+  JW_HIP_TRY(mem.alloc(&Z, (size_t)bc * Q * N * sizeof(cplx)));
+  JW_HIP_TRY(mem.alloc(&A, (size_t)bc * Q * N * sizeof(cplx)));
   for (long b0 = 0; b0 < batch && st == JW_OK; b0 += bc) {
     const long nb = std::min<long>(bc, batch - b0);
-    st = fft::run_fft<-1>(N, nb * (J + 1), RealIn{coeffs + b0 * (long)(J + 1) * N, N, N2},
-                          fft::SpecOut1{C, N, 0}, fft::SpecOut{C, N, N1, N2, 0}, A, s, T, false);
+    st = fft::run_fft<-1>(N, nb * Q, RealIn2{coeffs + b0 * (long)(J + 1) * N, N, N / N1n, J, Q},
+                          fft::SpecOut1{Z, N, 0}, fft::SpecOut{Z, N, N1n, N1, N2, 0}, A, s, T,
+                          false);
     if (st != JW_OK) break;
     const double inv = 1.0 / (double)N;
-    st = fft::run_fft<1>(N, nb, InvIn{C, R, N, N1, N2, J}, RealOut{x + b0 * N, N, 1, inv},
+    st = fft::run_fft<1>(N, nb, InvIn2{Z, P, N, N1, N2, Q}, RealOut{x + b0 * N, N, 1, inv},
                          RealOut{x + b0 * N, N, N1, inv}, A, s, T, false);
   }
   return st;
