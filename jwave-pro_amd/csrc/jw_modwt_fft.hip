@@ -13,6 +13,9 @@
 // (the reference's Bluestein lengths) run every length-N DFT as a chirp-z transform on it.
 #include <algorithm>
 #include <cmath>
+#include <map>
+#include <mutex>
+#include <utility>
 #include <vector>
 
 #include "jw_fft_passes.hpp"
@@ -181,11 +184,11 @@ __global__ void bs_post(const cplx* __restrict__ conv, cplx* __restrict__ out, c
 struct Bluestein {
   long N = 0, M = 0;
   Tables T;
-  cplx* w = nullptr;       // c_n, n < N
-  cplx* bh[2] = {};        // FFT_M(b) for S = -1 (index 0) and S = +1 (index 1)
-  cplx* ws = nullptr;      // 3 x items x M workspace: a, c and the inverse FFT's pass buffer
+  const cplx* w = nullptr;   // c_n, n < N (cached per device and N)
+  const cplx* bh[2] = {};    // FFT_M(b) for S = -1 (index 0) and S = +1 (index 1), cached
+  cplx* ws = nullptr;        // 3 x items x M workspace (the caller's StreamAllocs)
   long ws_items = 0;
-};  // device buffers owned by the caller's StreamAllocs
+};
 
 unsigned blocks(long n) { return (unsigned)((n + 255) / 256); }
 
@@ -215,39 +218,77 @@ int ifft_from_spec(long M, long items, const cplx* in, cplx* out, cplx* A, hipSt
                          NatOut{out, M, N1c}, A, s, T, false);
 }
 
+// c_n = e^{i pi n^2 / N}, the angle reduced exactly (n^2 mod 2N, n < 2^23 so n^2 < 2^46)
+__global__ void chirp_table(cplx* w, long N) {
+  const long n = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const long r = (n * n) % (2 * N);
+  double sn, cs;
+  sincospi((double)r / (double)N, &sn, &cs);
+  w[n] = make_double2(cs, sn);
+}
+// b for both signs, zero-padded to M: b_m = c_|m| (m < N, M - m < N), q = 1 conjugated
+__global__ void chirp_b(cplx* b, const cplx* w, long N, long M) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * M) return;
+  const long q = i / M, m = i - q * M;
+  const long j = m < N ? m : (M - m < N ? M - m : -1);
+  cplx c = j >= 0 ? w[j] : make_double2(0.0, 0.0);
+  if (q == 1) c.y = -c.y;
+  b[i] = c;
+}
+
+// The chirp tables and FFT_M(b) depend on N alone: built once per (device, N) on the device
+// (the first call for a length synchronises its stream once) and kept for the library's
+// lifetime, like the twiddle tables.
+std::mutex g_bs_mu;
+std::map<std::pair<int, long>, Bluestein> g_bs;
+
 int bluestein_init(Bluestein* B, long N, long max_items, StreamAllocs& mem, hipStream_t s) {
-  B->N = N;
-  B->M = 1;
-  while (B->M < 2 * N - 1) B->M <<= 1;
-  const long M = B->M;
-  int st = fft::tables(M, &B->T);
-  if (st != JW_OK) return st;
-  std::vector<cplx> hw(N);
-  const long double pi = 3.141592653589793238462643383279502884L;
-  for (long n = 0; n < N; ++n) {
-    const long r = (long)(((__int128)n * n) % (2 * N));  // e^{i pi n^2/N} = e^{i pi r/N}
-    const long double ang = pi * (long double)r / (long double)N;
-    hw[n] = make_double2((double)cosl(ang), (double)sinl(ang));
+  int dev = 0;
+  JW_HIP_TRY(hipGetDevice(&dev));
+  {
+    std::lock_guard<std::mutex> lk(g_bs_mu);
+    auto it = g_bs.find({dev, N});
+    if (it == g_bs.end()) {
+      Bluestein c;
+      c.N = N;
+      c.M = 1;
+      while (c.M < 2 * N - 1) c.M <<= 1;
+      const long M = c.M;
+      int st = fft::tables(M, &c.T);
+      if (st != JW_OK) return st;
+      cplx *w = nullptr, *bh = nullptr, *tmp = nullptr;
+      hipError_t e = hipMalloc((void**)&w, N * sizeof(cplx));
+      if (e == hipSuccess) e = hipMalloc((void**)&bh, 2 * M * sizeof(cplx));
+      if (e == hipSuccess) e = hipMalloc((void**)&tmp, 4 * M * sizeof(cplx));
+      if (e == hipSuccess) {
+        hipLaunchKernelGGL(chirp_table, dim3(blocks(N)), dim3(256), 0, s, w, N);
+        hipLaunchKernelGGL(chirp_b, dim3(blocks(2 * M)), dim3(256), 0, s, tmp, w, N, M);
+        e = hipGetLastError();
+      }
+      if (e == hipSuccess) {
+        st = fft_to_spec(M, 2, tmp, bh, tmp + 2 * M, s, c.T);  // column-major, as bs_mul
+        if (st == JW_OK) e = hipStreamSynchronize(s);
+      }
+      if (tmp) (void)hipFree(tmp);
+      if (e != hipSuccess || st != JW_OK) {
+        if (w) (void)hipFree(w);
+        if (bh) (void)hipFree(bh);
+        return st != JW_OK ? st
+                           : fail(JW_ERR_DEVICE, "chirp-z tables for N=%ld: %s", N,
+                                  hipGetErrorString(e));
+      }
+      c.w = w;
+      c.bh[0] = bh;
+      c.bh[1] = bh + M;
+      it = g_bs.emplace(std::make_pair(dev, N), c).first;
+    }
+    *B = it->second;
   }
   B->ws_items = max_items;
-  JW_HIP_TRY(mem.alloc(&B->w, N * sizeof(cplx)));
-  JW_HIP_TRY(mem.alloc(&B->bh[0], 2 * M * sizeof(cplx)));
-  B->bh[1] = B->bh[0] + M;
-  JW_HIP_TRY(mem.alloc(&B->ws, (size_t)3 * max_items * M * sizeof(cplx)));
-  JW_HIP_TRY(upload_async(B->w, hw.data(), N * sizeof(cplx), s));
-  // b_m for both signs, then their FFTs (two items of length M)
-  std::vector<cplx> hb(2 * M, make_double2(0.0, 0.0));
-  for (int q = 0; q < 2; ++q) {  // q = 0: S = -1 -> b = c; q = 1: S = +1 -> b = conj(c)
-    for (long m = 0; m < N; ++m) {
-      const cplx c = q == 0 ? hw[m] : make_double2(hw[m].x, -hw[m].y);
-      hb[q * M + m] = c;
-      if (m > 0) hb[q * M + M - m] = c;
-    }
-  }
-  cplx* tmp = B->ws;  // the workspace's first 2M entries stage b
-  JW_HIP_TRY(upload_async(tmp, hb.data(), 2 * M * sizeof(cplx), s));
-  // pass workspace: the next 2M entries (ws holds 2 x max_items x M, max_items = batch (J+1) >= 2)
-  return fft_to_spec(M, 2, tmp, B->bh[0], B->ws + 2 * M, s, B->T);  // column-major, as bs_mul
+  JW_HIP_TRY(mem.alloc(&B->ws, (size_t)3 * max_items * B->M * sizeof(cplx)));
+  return JW_OK;
 }
 
 // items length-N DFTs (S = -1 forward, +1 reverse without 1/N), natural order in -> out

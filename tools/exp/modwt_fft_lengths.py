@@ -13,7 +13,8 @@ sp = ctypes.c_void_p(s.cuda_stream)
 m = MODWTTransform(W.by_name("Daubechies4"))
 plan = m.initializeFilterCache()
 J, B = 8, 32
-for n in (1 << 20, 1000000, 1048577, 1 << 22, 4000000):
+LENGTHS = [int(a) for a in sys.argv[1:]] or [1 << 20, 1000000, 1048577, 1 << 22, 4000000]
+for n in LENGTHS:
     x = torch.empty((B, n), dtype=torch.float64, device=dev)
     _native.check(lib.jw_synth_uniform(ctypes.c_void_p(x.data_ptr()), n, B, 42, sp))
     c = torch.empty((B, J + 1, n), dtype=torch.float64, device=dev)
