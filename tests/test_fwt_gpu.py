@@ -86,11 +86,13 @@ def test_fwt2d_bit_exact(wname, rows, cols, lvlM, lvlN):
     (512, 64, 2, 6, "64"),      # every column level a strip: no tail
     (128, 64, 7, 6, "64"),      # one strip level
     (256, 64, 5, 6, "64"),      # tail with fewer levels than its length allows
-    (4096, 128, 12, 7, None),   # the cfg4 column geometry: 2 strips + 1024-row tail
+    (4096, 128, 12, 7, None),   # the cfg4 column geometry: levels 1-4 streamed + 256-row tail
+    (4096, 64, 4, 3, None),     # exactly the streamed levels: the level-4 approximations final
 ])
 def test_fwt2d_strip_columns_bit_exact(wname, rows, cols, lvlM, lvlN, tail, monkeypatch):
-    # tall matrices run the first column levels as row-strip kernels and the rest in an LDS
-    # tail (JW_FWT_TAIL shrinks the tail so small matrices take that path too)
+    # tall matrices run the first column levels as row-strip kernels (4096 rows and filters of
+    # up to 16 taps: the one-pass streaming kernel) and the rest in an LDS tail (JW_FWT_TAIL
+    # shrinks the tail so small matrices take that path too)
     if tail:
         monkeypatch.setenv("JW_FWT_TAIL", tail)
     wv = W.by_name(wname)
