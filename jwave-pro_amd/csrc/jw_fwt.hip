@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <utility>
 
+#include "jw_fwt_common.hpp"
 #include "jw_internal.hpp"
 
 namespace jw {
@@ -30,35 +31,10 @@ constexpr int kNT = 256;
 constexpr int kLdsN = 4096;              // signals up to this length run one workgroup each
 constexpr int kPer = kLdsN / kNT;        // outputs per thread per level (max)
 
-struct Filters {
-  double sD[kMaxTaps], wD[kMaxTaps], sR[kMaxTaps], wR[kMaxTaps];
-};
-
-template <bool FMA>
-__device__ __forceinline__ double madd(double acc, double f, double v) {
-  if constexpr (FMA) return __builtin_fma(f, v, acc);
-  else return acc + f * v;
-}
-
-template <bool FMA>
-__device__ __forceinline__ double contrib(double a, double d, double sr, double wr, int kind) {
-  double c;
-  if constexpr (FMA) c = __builtin_fma(a, sr, d * wr);
-  else c = (a * sr) + (d * wr);
-  return kind == JW_WAVELET_HAAR_ORTH ? .5 * c : c;
-}
-
-// acc + contrib: STRICT keeps Java's acc + ((a*sR) + (d*wR)); FMA folds both products into
-// the running sum, fma(d, wR, fma(a, sR, acc)) -- same taps, same order, 2 instead of 3
-// double ops per tap pair (the reverse cascades are VALU-heavy).
-template <bool FMA, int KIND>
-__device__ __forceinline__ double rev_acc(double acc, double a, double d, double sr, double wr) {
-  if constexpr (FMA && KIND != JW_WAVELET_HAAR_ORTH) {
-    return __builtin_fma(d, wr, __builtin_fma(a, sr, acc));
-  } else {
-    return acc + contrib<FMA>(a, d, sr, wr, KIND);
-  }
-}
+using fwtc::Filters;
+using fwtc::madd;
+using fwtc::contrib;
+using fwtc::rev_acc;
 
 // Wavelet.forward output pair (i, i + h/2) from in[0..h).
 template <bool FMA>
@@ -703,113 +679,6 @@ __global__ __launch_bounds__(256) void fwt_strip_rev(Strip s, Filters f) {
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Streaming column forward: levels 1..S of 64 columns per wavefront in ONE pass over HBM
-// (the strip kernels above take one pass per level).  Lane l owns column c0 + l and walks it
-// top to bottom; every row read is a 512-byte coalesced piece.  Level k keeps its last 16
-// inputs in registers (a ring indexed by stream position mod 16); output pair i of level k is
-// produced as soon as input 2i + M - 1 arrives, its detail goes straight to its final row
-// h_k/2 + i, its approximation feeds level k+1 (level S: row i, the tail's input).
-// Circularity without saving anything: the level-1 stream simply runs past the bottom of the
-// column (row p mod rows) for E = sum of the levels' look-ahead (210 rows for M = 16, S = 4),
-// so every level sees its first inputs again at the end and computes its wrapped outputs
-// then; the few outputs computed twice are written twice with identical values.
-// Reads T (the row pass's output), writes y: the column cannot be updated in place (detail
-// row h/2 + i is written long before row h/2 + i is read).  Same sums, same order as
-// Wavelet.forward per column (bit-identical in STRICT).
-// Every ring slot is a compile-time register: positions advance by known amounts per
-// macro-step of 2^S rows, and 2^(S-1) macro-steps are unrolled per loop trip.
-// ---------------------------------------------------------------------------------------
-constexpr int kStreamRing = 16;  // taps per level kept in registers (filters up to 16 taps)
-
-struct StreamCtx {
-  double* dst;   // y + matrix + column
-  long cols;
-  long p0;       // level-1 stream position of the current loop trip (multiple of 2^(2S-1))
-  int rows;
-};
-
-constexpr int smod(int q) { return ((q % kStreamRing) + kStreamRing) % kStreamRing; }
-
-template <bool FMA, int M, int S, int K, int Q>
-__device__ __forceinline__ void stream_feed(double (&ring)[S][kStreamRing], double v,
-                                            const StreamCtx& c, const Filters& f) {
-  // level K input at stream position (p0 >> (K-1)) + Q
-  ring[K - 1][smod(Q)] = v;
-  if constexpr ((Q & 1) != 0 && (Q - M + 1) % 2 == 0) {
-    constexpr int O = (Q - M + 1) / 2;  // output pair (p0 >> K) + O is complete
-    double lo = 0., hi = 0.;
-#pragma unroll
-    for (int t = 0; t < M; ++t) {
-      const double x = ring[K - 1][smod(2 * O + t)];
-      lo = madd<FMA>(lo, f.sD[t], x);
-      hi = madd<FMA>(hi, f.wD[t], x);
-    }
-    const long i = (c.p0 >> K) + O;
-    const int hk = c.rows >> (K - 1), halfk = hk >> 1;
-    if (i >= 0) c.dst[(long)(halfk + (i & (halfk - 1))) * c.cols] = hi;
-    if constexpr (K < S) {
-      stream_feed<FMA, M, S, K + 1, O>(ring, lo, c, f);
-    } else {
-      if (i >= 0) c.dst[(long)(i & (halfk - 1)) * c.cols] = lo;
-    }
-  }
-}
-
-template <bool FMA, int M, int S, int U0, int... Js>
-__device__ __forceinline__ void stream_macro(double (&ring)[S][kStreamRing],
-                                             const double (&in)[1 << S], const StreamCtx& c,
-                                             const Filters& f, std::integer_sequence<int, Js...>) {
-  (stream_feed<FMA, M, S, 1, U0 * (1 << S) + Js>(ring, in[Js], c, f), ...);
-}
-
-template <bool FMA, int M, int S, int... Us>
-__device__ __forceinline__ void stream_trip(double (&ring)[S][kStreamRing], double (&in)[1 << S],
-                                            const double* src, long cols, int rows, StreamCtx& c,
-                                            const Filters& f, std::integer_sequence<int, Us...>) {
-  constexpr int MS = 1 << S;
-  auto one = [&](auto uc) {
-    constexpr int U = decltype(uc)::value;
-    double nx[MS];  // the next macro-step's rows, in flight behind this one
-    const long nb = c.p0 + (long)(U + 1) * MS;
-#pragma unroll
-    for (int j = 0; j < MS; ++j) nx[j] = src[((nb + j) & (rows - 1)) * cols];
-    stream_macro<FMA, M, S, U>(ring, in, c, f, std::make_integer_sequence<int, MS>{});
-#pragma unroll
-    for (int j = 0; j < MS; ++j) in[j] = nx[j];
-  };
-  (one(std::integral_constant<int, Us>{}), ...);
-}
-
-// 8 macro-steps per trip: the trip start p0 is then a multiple of 2^(S+3), so every level's
-// stream position (p0 >> (K-1)) is a multiple of the ring size.
-constexpr int kStreamUnroll = 8;
-
-template <bool FMA, int M, int S>
-__global__ __launch_bounds__(64) void fwt_cols_stream_fwd(const double* __restrict__ T,
-                                                          double* __restrict__ y, int rows,
-                                                          int cols, long mstride, long trips,
-                                                          Filters f) {
-  static_assert(M <= kStreamRing && M % 2 == 0, "streamed filters: even, <= 16 taps");
-  constexpr int MS = 1 << S, UN = kStreamUnroll;
-  const long col = (long)blockIdx.x * 64 + threadIdx.x;
-  const double* src = T + (long)blockIdx.y * mstride + col;
-  StreamCtx c{y + (long)blockIdx.y * mstride + col, (long)cols, 0L, rows};
-  double ring[S][kStreamRing];
-#pragma unroll
-  for (int k = 0; k < S; ++k)
-#pragma unroll
-    for (int q = 0; q < kStreamRing; ++q) ring[k][q] = 0.;
-  double in[MS];
-#pragma unroll
-  for (int j = 0; j < MS; ++j) in[j] = src[(long)(j & (rows - 1)) * cols];
-  for (long t = 0; t < trips; ++t) {
-    stream_trip<FMA, M, S>(ring, in, src, (long)cols, rows, c, f,
-                           std::make_integer_sequence<int, UN>{});
-    c.p0 += (long)UN * MS;
-  }
-}
-
 // The remaining levels of kTailNL columns on rows [0, len) (len <= kTailLen), in LDS:
 // forward levels lvl_h0 = level count from h = len; reverse from h = lvl_h0 up to len.
 template <bool FMA, int M, bool REV, int KIND>
@@ -986,29 +855,6 @@ bool launch_strip(int M, int kind, bool rev, hipStream_t s, const Strip& st, int
       hipLaunchKernelGGL((fwt_strip_rev<FMA, MM, JW_WAVELET_GENERIC>), g, b, 0, s, st, f);    \
     return true;
     JW_STRIP_LENGTHS(JW_C)
-#undef JW_C
-    default:
-      return false;
-  }
-}
-
-// Streaming forward column pass (S = 4 levels, filters of up to 16 taps): T -> y.
-template <bool FMA>
-bool launch_stream_fwd(int M, int S, hipStream_t s, const double* T, double* y, int rows,
-                       int cols, long mat, int batch, const Filters& f) {
-  const char* e = std::getenv("JW_FWT_STREAM");
-  if ((e && e[0] == '0') || S != 4 || M > kStreamRing || M % 2 || cols % 64) return false;
-  const long E = ((1L << S) - 1) * (M - 2);           // look-ahead of the S levels, in rows
-  const long trip = (long)kStreamUnroll << S;         // rows per loop trip
-  const long trips = (rows + E + trip - 1) / trip;
-  const dim3 g((unsigned)(cols / 64), (unsigned)batch), b(64);
-  switch (M) {
-#define JW_C(MM)                                                                            \
-  case MM:                                                                                  \
-    hipLaunchKernelGGL((fwt_cols_stream_fwd<FMA, MM, 4>), g, b, 0, s, T, y, rows, cols, mat, \
-                       trips, f);                                                           \
-    return true;
-    JW_C(2) JW_C(4) JW_C(6) JW_C(8) JW_C(10) JW_C(12) JW_C(14) JW_C(16)
 #undef JW_C
     default:
       return false;
@@ -1276,7 +1122,7 @@ int fwt2d_forward_strips(const FwtPlan& p, int S, const double* x, double* y, in
   const Filters f = make_filters(p);
   const int tail_lv = lvlM - S;
   // levels 1..4 of every column in one pass (T -> y), then the tail in place on y
-  if (st == JW_OK && launch_stream_fwd<FMA>(p.M, S, s, T, y, rows, cols, mat, batch, f)) {
+  if (st == JW_OK && fwtc::launch_stream_fwd<FMA>(p.M, S, s, T, y, rows, cols, mat, batch, f)) {
     if (tail_lv > 0 && !launch_tail<FMA>(p.M, p.kind, false, s, y, y, rows >> S, cols, mat, mat,
                                          tail_lv, p.tw, batch, f))
       st = fail(JW_ERR_UNSUPPORTED, "no 2-D strip kernel for filter length %d", p.M);
@@ -1312,9 +1158,12 @@ int fwt2d_reverse_strips(const FwtPlan& p, int S, const double* y, double* x, in
   JW_HIP_TRY(mem.alloc(&B, sizeof(double) * half * batch));
   const Filters f = make_filters(p);
   const int tail_lv = lvlM - S;
-  // level l (h = rows >> l) writes rows [0, h) of O_l: O_0 = T, then alternating with B
-  auto obuf = [&](int l) { return (l & 1) ? B : T; };
-  auto oms = [&](int l) { return (l & 1) ? half : mat; };
+  // level l (h = rows >> l) writes rows [0, h) of O_l: O_0 = T, then alternating with B.
+  // The streaming pass writes T from the tail's output, so that output goes to B then.
+  const bool stream = fwtc::launch_stream_rev<FMA>(p.M, p.kind, S, s, nullptr, 0, nullptr,
+                                                   nullptr, rows, cols, mat, batch, f);
+  auto obuf = [&](int l) { return stream && l == S ? B : (l & 1) ? B : T; };
+  auto oms = [&](int l) { return stream && l == S ? half : (l & 1) ? half : mat; };
   int st = JW_OK;
   const double* a = y;  // approximations of the next (finer) level
   long ms_a = mat;
@@ -1326,6 +1175,12 @@ int fwt2d_reverse_strips(const FwtPlan& p, int S, const double* y, double* x, in
       st = fail(JW_ERR_UNSUPPORTED, "no 2-D strip kernel for filter length %d", p.M);
     a = obuf(S);
     ms_a = oms(S);
+  }
+  // levels 4..1 of every column in one pass (a + the details of y -> T)
+  if (st == JW_OK && stream &&
+      fwtc::launch_stream_rev<FMA>(p.M, p.kind, S, s, a, ms_a, y, T, rows, cols, mat, batch, f)) {
+    JW_HIP_TRY(hipGetLastError());
+    return fwt_reverse_device(p, T, x, cols, lvlN, rows * batch, s);  // rows
   }
   for (int l = S - 1; l >= 0 && st == JW_OK; --l) {
     const int h = rows >> l;
