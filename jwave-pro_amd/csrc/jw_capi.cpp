@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -31,6 +32,21 @@ int fail(int code, const char* fmt, ...) {
 }
 
 void clear_error() { g_err[0] = '\0'; }
+
+void keep_pool_memory() {
+  static std::mutex mu;
+  static bool done[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
+  std::lock_guard<std::mutex> lk(mu);
+  if (done[dev]) return;
+  done[dev] = true;
+  hipMemPool_t pool = nullptr;
+  if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess && pool) {
+    uint64_t keep = UINT64_MAX;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+  }
+}
 
 namespace {
 

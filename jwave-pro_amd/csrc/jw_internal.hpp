@@ -27,6 +27,12 @@ void clear_error();
                         __FILE__, __LINE__);                                               \
   } while (0)
 
+// The device's default memory pool keeps what the workspaces free instead of returning it to
+// the driver at every synchronisation (the default release threshold is 0): without this a
+// call whose workspace is several GB (the 2-D FWT of cfg4: 6.4 GB) re-maps it every time,
+// ~200 ms per call on some boxes.  Set once per device, on first use.
+void keep_pool_memory();
+
 // Stream-ordered device allocations of one call, released on every exit path (the early
 // returns of JW_HIP_TRY included): hipFreeAsync on the call's stream, so the memory is
 // reused only after the work queued on that stream has consumed it.
@@ -42,6 +48,7 @@ class StreamAllocs {
   hipError_t alloc(T** out, size_t bytes) {
     *out = nullptr;
     if (n_ == kMax) return hipErrorOutOfMemory;
+    keep_pool_memory();
     void* p = nullptr;
     const hipError_t e = hipMallocAsync(&p, bytes, s_);
     if (e == hipSuccess) {
