@@ -16,6 +16,6 @@ for k in "${KS[@]}"; do
   python3 -c "
 import json
 d=json.loads([l for l in open('gpurun_out/ab_${TAG}_$i_$k.log') if l.startswith('{')][-1])
-r=d['roofline']; o=d.get('other_arith',{})
+r=d['roofline']; o=d.get('other_arith') or {}
 print('$i $k', d['value'], d['ms_per_step'], 'fwd', r['fwd_ms'], 'inv', r['inv_ms'], d.get('spot_check_vs_oracle'), 'strict inv', o.get('inv_ms'), o.get('spot_check_vs_oracle'))"
 done
