@@ -31,6 +31,7 @@ using fft::ColOut;
 using fft::RowIn;
 using fft::SpecOut;
 using fft::SpecOut1;
+using fft::SpecOutBoth;
 using fft::nt_store;
 using fft::run_fft;
 using fft::tpos;
@@ -132,6 +133,62 @@ struct PadIn {  // padded real signal, element k (padSignal :269-306)
     return make_double2(v, 0.0);
   }
 };
+// psi_hat of (scale s, bin k) exactly as the inverse FFT's first pass uses it: for Morlet and
+// Mexican hat the per-bin divisions hoisted into per-scale constants: the bin's signed index
+// kk = k or k - N (createFrequencyAxis :453-456) times
+//   Morlet:      f = a*omega/(2 pi) = kk * (a fs / N)            (MorletWavelet :114-124)
+//   Mexican hat: a*omega = kk * (2 pi a fs / N)                  (MexicanHatWavelet :107-119)
+// (a few ulps from the reference's operation order; the tests bound it at 1e-12).
+// sc: per scale {bin step, norm * sqrt(a)}, see cwt_fft_device.
+template <int K>
+__device__ __forceinline__ cplx psi_bin(const WaveletFT& w, const double* scales, const double* sc,
+                                        int s, long k, long N, double fs) {
+  if constexpr (K == JW_CWT_MORLET || K == JW_CWT_MEXHAT) {
+    const double kk = (double)(k > N / 2 ? k - N : k);
+    const double step = sc[2 * s], amp = sc[2 * s + 1];
+    double e, m = amp;
+    if constexpr (K == JW_CWT_MORLET) {
+      const double d = kk * step - w.p1;
+      e = w.p2 * d * d;  // p2 = -2 pi^2 fb
+    } else {
+      const double om = kk * step, om2 = om * om;
+      e = w.p2 * om2;  // p2 = -0.5 sigma^2
+      m *= om2;
+    }
+    // Bins past the underflow point are exact zeros (as Math.exp gives): no exp, no X
+    // read.  A narrow band leaves whole 64-bin wave blocks zero, so the branch skips them.
+    if (e < -746.0) return make_double2(0.0, 0.0);
+    return make_double2(m * exp(e), 0.0);
+  } else {
+    double om = 2.0 * kPi * (double)k * fs / (double)N;  // createFrequencyAxis :453-456
+    if (k > N / 2) om -= 2.0 * kPi * fs;
+    const double a = scales[s];
+    return psi_hat<K>(w, om, a, sqrt(a));
+  }
+}
+
+// Pair q of a (sub)set of the (signal, scale) pairs: signal q / nsub, scale smap[q % nsub]
+// (smap == nullptr: all ns scales, q = signal * ns + scale).
+// Pair counts stay below 2^31 (checked on the host): 32-bit division, which the scalar unit
+// does in a fraction of the 64-bit sequence.
+struct PairMap {
+  const int* smap;
+  int nsub, ns;
+  __device__ __forceinline__ void split(long q, long& sig, int& s) const {
+    const unsigned uq = (unsigned)q, un = (unsigned)nsub, sg = uq / un;
+    const int r = (int)(uq - sg * un);
+    sig = sg;
+    s = smap ? smap[r] : r;
+  }
+  __device__ __forceinline__ long out_pair(long q) const {  // signal * ns + scale
+    if (!smap) return q;
+    long sig;
+    int s;
+    split(q, sig, s);
+    return sig * ns + s;
+  }
+};
+
 template <int K>
 struct ScaleIn {  // X[sig][k] * conj(psi_hat(omega_k, a_s)), k = N2 k1 + col; item = pair in group
   static constexpr bool kStrided = false;  // column-major spectra: contiguous columns
@@ -139,41 +196,15 @@ struct ScaleIn {  // X[sig][k] * conj(psi_hat(omega_k, a_s)), k = N2 k1 + col; i
   const double* scales;
   WaveletFT w;
   long N, N1, N2, pair0;
-  int ns;
+  PairMap pm;
   double fs;
   const double* sc;  // per scale (MORLET, MEXHAT): {bin step, norm * sqrt(a)}, see cwt_fft_device
   __device__ cplx operator()(long item, long k1, long col) const {
-    const long p = pair0 + item, sig = p / ns;
-    const int s = (int)(p - sig * ns);
+    long sig;
+    int s;
+    pm.split(pair0 + item, sig, s);
     const long k = N2 * k1 + col;
-    cplx wv;
-    if constexpr (K == JW_CWT_MORLET || K == JW_CWT_MEXHAT) {
-      // The same spectra with the per-bin divisions hoisted into per-scale constants: the
-      // bin's signed index kk = k or k - N (createFrequencyAxis :453-456) times
-      //   Morlet:      f = a*omega/(2 pi) = kk * (a fs / N)            (MorletWavelet :114-124)
-      //   Mexican hat: a*omega = kk * (2 pi a fs / N)                  (MexicanHatWavelet :107-119)
-      // (a few ulps from the reference's operation order; the tests bound it at 1e-12).
-      const double kk = (double)(k > N / 2 ? k - N : k);
-      const double step = sc[2 * s], amp = sc[2 * s + 1];
-      double e, m = amp;
-      if constexpr (K == JW_CWT_MORLET) {
-        const double d = kk * step - w.p1;
-        e = w.p2 * d * d;  // p2 = -2 pi^2 fb
-      } else {
-        const double om = kk * step, om2 = om * om;
-        e = w.p2 * om2;  // p2 = -0.5 sigma^2
-        m *= om2;
-      }
-      // Bins past the underflow point are exact zeros (as Math.exp gives): no exp, no X
-      // read.  A narrow band leaves whole 64-bin wave blocks zero, so the branch skips them.
-      if (e < -746.0) return make_double2(0.0, 0.0);
-      wv = make_double2(m * exp(e), 0.0);
-    } else {
-      double om = 2.0 * kPi * (double)k * fs / (double)N;  // createFrequencyAxis :453-456
-      if (k > N / 2) om -= 2.0 * kPi * fs;
-      const double a = scales[s];
-      wv = psi_hat<K>(w, om, a, sqrt(a));
-    }
+    const cplx wv = psi_bin<K>(w, scales, sc, s, k, N, fs);
     if (wv.x == 0.0 && wv.y == 0.0) return make_double2(0.0, 0.0);  // skip the X read
     const cplx xv = X[sig * N + col * N1 + k1];
     if constexpr (K == JW_CWT_DOG || K == JW_CWT_MEYER) {
@@ -189,10 +220,12 @@ struct CoefOut {  // out[pair][t] = v / N for t = line + N1 * idx < n  (reverse 
   long n, N1, pair0;
   double inv_n;
   bool nt;
+  PairMap pm;  // item -> (signal, scale) of the output
   __device__ void operator()(long item, long idx, long line, cplx v) const {
     const long t = line + N1 * idx;
+    const long pr = pm.out_pair(pair0 + item);  // outside the branch: hoisted per workgroup
     if (t < n) {
-      cplx* o = (cplx*)(out + 2 * ((pair0 + item) * n + t));
+      cplx* o = (cplx*)(out + 2 * (pr * n + t));
       const cplx r = make_double2(v.x * inv_n, v.y * inv_n);
       if (nt) {
         nt_store(o, r);
@@ -204,7 +237,175 @@ struct CoefOut {  // out[pair][t] = v / N for t = line + N1 * idx < n  (reverse 
 };
 
 
+// ---------------------------------------------------------------------------------------
+// Band-limited scales in one pass.  With N = N1 x 512 (input k = 512 k1 + k2, output
+// t = n1 + N1 n2) the inverse FFT's row n1 is the 512-point FFT over k2 of
+//   A[n1][k2] = W_N^(n1 k2) sum_k1 Z[512 k1 + k2] W_N1^(k1 n1),   Z = X conj(psi_hat).
+// For a large scale, psi_hat is above e^-60 of its peak only in a few consecutive 512-bin
+// blocks k1 = b0 .. b0 + nb - 1 (mod N1); below that it lies ten orders of magnitude under the
+// rounding of the spectrum X itself, and those bins are dropped.  A[n1][.] then costs nb
+// complex multiply-adds per element, computed in registers from the band, so the row needs
+// no workspace: one pass, 16 B written per output and 24 B read per band bin (L2-resident).
+// ---------------------------------------------------------------------------------------
+constexpr double kBandE = 60.0;  // bins with |psi_hat| < e^-60 |psi_hat|max are dropped
+
+struct BandScale {
+  long b0;       // first 512-bin block of the band (mod N1)
+  long psi_off;  // offset of this scale's psi_hat band in the table (nb x 512 entries)
+  int nb;        // blocks in the band
+  int s;         // scale index
+};
+
+// psi_hat of every bin of every band block, as the two-pass path evaluates it (psi_bin)
+template <int K>
+__global__ __launch_bounds__(256) void cwt_band_psi(const BandScale* bands, double* psi,
+                                                    WaveletFT w, const double* scales,
+                                                    const double* sc, long N, long N1, double fs) {
+  const BandScale b = bands[blockIdx.y];
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long)b.nb * 512) return;
+  const long k = 512 * ((b.b0 + (e >> 9)) & (N1 - 1)) + (e & 511);
+  psi[b.psi_off + e] = psi_bin<K>(w, scales, sc, b.s, k, N, fs).x;
+}
+
+// e^{+2 pi i m / N1} = W_N^(512 m), m < N1: the band kernel's wave-uniform twiddles
+// stored as {cos, sin, cos + sin, 0} for the three-product complex multiply-add (Gauss)
+__global__ __launch_bounds__(256) void cwt_band_roots(double4* w, long N, long N1, Tables T) {
+  const long m = (long)blockIdx.x * 256 + threadIdx.x;
+  if (m < N1) {
+    const cplx r = fft::twiddle(T, 512 * m);
+    w[m] = make_double4(r.x, r.y, r.x + r.y, 0.0);
+  }
+}
+
+// One workgroup = 8 consecutive rows n1 of one band pair (sig, band scale): thread k2 sums the
+// band for all 8 rows, the rows go through the tile into the wavefront FFT (one row per wave)
+// and leave as 8-row (128-byte) output pieces.  Xn: natural-order spectra.  The twiddles
+// W_N1^(k1 n1) are uniform over the workgroup: scalar loads from the N1-entry root table.
+// Placement: the rpp = N1/8 workgroups of a pair share blockIdx % 8 (one XCD under the
+// round-robin dispatch), so the pair's band of X is fetched into one L2, not eight (speed only).
+__global__ __launch_bounds__(512) void cwt_band512(const cplx* __restrict__ Xn,
+                                                   const double* __restrict__ psi,
+                                                   const BandScale* __restrict__ bands, int nband,
+                                                   const double4* __restrict__ wN1, long N, long N1,
+                                                   long items, CoefOut out, Tables T) {
+  __shared__ cplx tile[fft::kTile];
+  // 32-bit index math (the scalar unit runs 64-bit division as a ~100-instruction sequence)
+  const unsigned lrpp = (unsigned)__builtin_ctzl(N1 / fft::kT), local = blockIdx.x >> 3;
+  const unsigned slot = local >> lrpp;
+  const unsigned item = slot * 8 + (blockIdx.x & 7);
+  const unsigned rg = local - (slot << lrpp);
+  if (item >= (unsigned long)items) return;
+  const long r0 = (long)rg * fft::kT;
+  const unsigned sig = item / (unsigned)nband;
+  const BandScale b = bands[item - sig * (unsigned)nband];
+  // thread (h, kp): columns kp and kp + 256, rows r0 + 4h .. r0 + 4h + 3 (h uniform per wave,
+  // so each wave-uniform twiddle feeds two columns)
+  const int tid = threadIdx.x, lane = tid & 63, c = tid >> 6, h = tid >> 8, kp = tid & 255;
+  const unsigned m1 = (unsigned)N1 - 1;
+  const unsigned rr = __builtin_amdgcn_readfirstlane((unsigned)r0 + 4 * h);  // wave-uniform
+  // sum_j z w as three real sums (Gauss): s1 = sum zr c, s2 = sum zi d, s3 = sum (zr+zi)(c+d);
+  // re = s1 - s2, im = s3 - s1 - s2: three multiply-adds per term instead of four
+  double s1[2][4], s2[2][4], s3[2][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) s1[q][t] = s2[q][t] = s3[q][t] = 0.0;
+  const cplx* xs = Xn + (long)sig * N + kp;
+  const double* ps = psi + b.psi_off + kp;
+  constexpr int kU = 4;  // blocks whose loads are in flight together
+  for (int j0 = 0; j0 < b.nb; j0 += kU) {
+    cplx xv[kU][2];
+    double p[kU][2];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int j = j0 + u < b.nb ? j0 + u : b.nb - 1;  // clamped; skipped below
+      const unsigned k1 = ((unsigned)b.b0 + j) & m1;
+      xv[u][0] = xs[512 * k1];
+      xv[u][1] = xs[512 * k1 + 256];
+      p[u][0] = ps[512 * j];
+      p[u][1] = ps[512 * j + 256];
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (j0 + u >= b.nb) break;
+      const unsigned k1 = ((unsigned)b.b0 + j0 + u) & m1;
+      double zr[2], zi[2], zs[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        zr[q] = xv[u][q].x * p[u][q];
+        zi[q] = xv[u][q].y * p[u][q];
+        zs[q] = zr[q] + zi[q];
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const double4 w = wN1[(k1 * (rr + t)) & m1];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          s1[q][t] = fma(zr[q], w.x, s1[q][t]);
+          s2[q][t] = fma(zi[q], w.y, s2[q][t]);
+          s3[q][t] = fma(zs[q], w.z, s3[q][t]);
+        }
+      }
+    }
+  }
+  // four-step twiddle W_N^(n1 k2), then row n1 - r0 of the tile: for column kp
+  // W_N^((rr + t) kp) = W_N^(rr kp) (W_N^kp)^t (two lookups per lane, three products), for
+  // column kp + 256 times the wave-uniform W_N^(256 (rr + t))
+  cplx w0 = fft::twiddle(T, ((long)rr * kp) & (N - 1));
+  const cplx st = fft::twiddle(T, kp);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const cplx u = fft::twiddle(T, (256L * (rr + t)) & (N - 1));  // uniform: scalar loads
+    const cplx v0 = make_double2(s1[0][t] - s2[0][t], s3[0][t] - s1[0][t] - s2[0][t]);
+    const cplx v1 = make_double2(s1[1][t] - s2[1][t], s3[1][t] - s1[1][t] - s2[1][t]);
+    tile[(4 * h + t) * 512 + kp] = fft::cmul(v0, w0);
+    tile[(4 * h + t) * 512 + kp + 256] = fft::cmul(v1, fft::cmul(w0, u));
+    if (t < 3) w0 = fft::cmul(w0, st);
+  }
+  __syncthreads();
+  cplx a[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) a[r] = tile[c * 512 + lane + 64 * r];
+  __syncthreads();
+  CoefOut o = out;
+  o.pair0 = (long)sig * out.pm.ns + b.s;  // one output pair per workgroup
+  fft::pass512_tail<1, false>(a, o, N, 512L, T, 0L, r0, tile);
+}
+
 }  // namespace
+
+// The band of scale a (bins whose psi_hat is above e^-kBandE of its peak) as 512-bin blocks
+// b0 .. b0 + nb - 1 mod N1; false when the band is not known in closed form (Paul, DOG,
+// Meyer) or wraps the whole spectrum.  Morlet: |f - fc| <= sqrt(E / (2 pi^2 fb)) with
+// f = kk a fs / N; Mexican hat: u = sigma^2 om^2 / 2 with u - ln u <= E + 1 (om^2 e^-u
+// against its peak 2/(e sigma^2)), om = 2 pi kk a fs / N.  Two bins of margin each side.
+static bool cwt_band(int wavelet, const WaveletFT& w, double a, double fs, long N, long* b0,
+                     int* nb) {
+  double lo, hi;
+  if (wavelet == JW_CWT_MORLET) {
+    const double step = a * fs / (double)N;
+    if (!(w.p0 > 0) || !(step > 0)) return false;
+    const double d = std::sqrt(kBandE / (2.0 * kPi * kPi * w.p0));
+    lo = std::floor((w.p1 - d) / step) - 2;
+    hi = std::ceil((w.p1 + d) / step) + 2;
+  } else if (wavelet == JW_CWT_MEXHAT) {
+    const double step = 2.0 * kPi * a * fs / (double)N;
+    if (!(w.p0 > 0) || !(step > 0)) return false;
+    const double u = kBandE + 2.0 + std::log(kBandE + 1.0 + std::log(kBandE + 1.0));
+    const double W = std::ceil(std::sqrt(2.0 * u) / w.p0 / step) + 2;
+    lo = -W;
+    hi = W;
+  } else {
+    return false;
+  }
+  if (!(lo > -(double)(N / 2)) || !(hi < (double)(N / 2))) return false;
+  const long blo = (long)std::floor(lo / 512.0), bhi = (long)std::floor(hi / 512.0);
+  const long N1 = N / 512;
+  *nb = (int)(bhi - blo + 1);
+  *b0 = ((blo % N1) + N1) % N1;
+  return true;
+}
 
 // Group sizes: signals per forward chunk and (signal, scale) pairs per inverse group, so the
 // workspace A stays ~128 MB (Infinity Cache sized) at N = 2^18.
@@ -215,6 +416,8 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   long N = 1;
   while (N < n) N <<= 1;  // MathUtils.nextPowerOfTwo :46-49
   if (N > (1L << 24)) return fail(JW_ERR_UNSUPPORTED, "CWT padded length %ld > 2^24", N);
+  if ((long)batch * ns >= (1L << 31))
+    return fail(JW_ERR_UNSUPPORTED, "CWT batch x scales = %ld >= 2^31", (long)batch * ns);
   Tables T;
   int st = fft::tables(N, &T);
   if (st != JW_OK) return st;
@@ -244,17 +447,46 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   }
   const char* gnt = std::getenv("JW_CWT_NT");  // A/B runs: bit 1 = NT stores of A, 2 = of coeffs
   const int ntm = gnt ? std::atoi(gnt) : 2;  // measured best: NT coefficient stores only
+  w.p2 = wavelet == JW_CWT_MORLET ? -2.0 * kPi * kPi * w.p0 : -0.5 * w.p0 * w.p0;
+  // Scales whose band spans at most nbmax 512-bin blocks run in one pass (cwt_band512); the
+  // rest through the two-pass FFT.  One pass costs ~1.1 us per (signal, scale) pair at N = 2^18
+  // plus ~0.05 us per block, two passes ~3 us: the measured optimum at cfg3 is nbmax = 32
+  // (profiles/r02/cwt_band_sweep_r02.log).  env JW_CWT_BAND (A/B runs): nbmax, 0 = all two-pass.
+  const char* gbd = std::getenv("JW_CWT_BAND");
+  const int nbmax = gbd ? std::atoi(gbd) : 32;
+  const long N1b = N / 512;
+  std::vector<BandScale> bands;
+  std::vector<int> full;
+  long psi_total = 0;
+  int nb_hi = 0;
+  for (int i = 0; i < ns; ++i) {
+    long b0 = 0;
+    int nb = 0;
+    if (N >= 8192 && nbmax > 0 && cwt_band(wavelet, w, scales_host[i], fs, N, &b0, &nb) &&
+        nb <= nbmax && nb <= N1b) {
+      bands.push_back(BandScale{b0, psi_total, nb, i});
+      psi_total += 512L * nb;
+      nb_hi = std::max(nb_hi, nb);
+    } else {
+      full.push_back(i);
+    }
+  }
+  const int nband = (int)bands.size(), nfull = (int)full.size();
   const char* gmb = std::getenv("JW_CWT_GROUP_MB");  // A/B runs: workspace size in MiB
   const long ws = (gmb ? std::atol(gmb) : 128L) << 20;
   const long per = std::max(1L, ws / (N * (long)sizeof(cplx)));
-  const long gsig = std::min<long>(batch, per), gpair = std::min<long>((long)batch * ns, per);
+  const long pairs = (long)batch * nfull;  // two-pass pairs
+  const long gsig = std::min<long>(batch, per), gpair = std::max(1L, std::min<long>(pairs, per));
   // N = 2^18 (512 x 512): the pairs' inverse FFTs are software-pipelined over two workspaces
   // (run_fft512_pipelined); env JW_CWT_PIPE=0 runs the groups one after the other (A/B runs).
   const char* gpp = std::getenv("JW_CWT_PIPE");
-  const bool pipe = N == (1L << 18) && (long)batch * ns > gpair && !(gpp && gpp[0] == '0');
+  const bool pipe = N == (1L << 18) && pairs > gpair && !(gpp && gpp[0] == '0');
   StreamAllocs mem(s);
-  cplx *X = nullptr, *A = nullptr;
-  double* dsc = nullptr;
+  cplx *X = nullptr, *A = nullptr, *Xn = nullptr;
+  double4* wN1 = nullptr;
+  double *dsc = nullptr, *psi = nullptr;
+  BandScale* dbands = nullptr;
+  int* dsmap = nullptr;
   const long a_items = std::max(gsig, pipe ? 2 * gpair : gpair);
   JW_HIP_TRY(mem.alloc(&X, (size_t)batch * N * sizeof(cplx)));
   JW_HIP_TRY(mem.alloc(&A, (size_t)a_items * N * sizeof(cplx)));
@@ -266,28 +498,67 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     hsc[ns + 2 * i] = wavelet == JW_CWT_MEXHAT ? 2.0 * kPi * a * fs / (double)N : a * fs / (double)N;
     hsc[ns + 2 * i + 1] = w.norm * std::sqrt(a);
   }
-  w.p2 = wavelet == JW_CWT_MORLET ? -2.0 * kPi * kPi * w.p0 : -0.5 * w.p0 * w.p0;
   JW_HIP_TRY(mem.alloc(&dsc, hsc.size() * sizeof(double)));
   JW_HIP_TRY(upload_async(dsc, hsc.data(), hsc.size() * sizeof(double), s));
+  if (nband > 0) {
+    JW_HIP_TRY(mem.alloc(&Xn, (size_t)batch * N * sizeof(cplx)));
+    JW_HIP_TRY(mem.alloc(&psi, (size_t)psi_total * sizeof(double)));
+    JW_HIP_TRY(mem.alloc(&wN1, (size_t)N1b * sizeof(double4)));
+    JW_HIP_TRY(mem.alloc(&dbands, bands.size() * sizeof(BandScale)));
+    JW_HIP_TRY(upload_async(dbands, bands.data(), bands.size() * sizeof(BandScale), s));
+  }
+  if (nfull > 0 && nfull < ns) {
+    JW_HIP_TRY(mem.alloc(&dsmap, full.size() * sizeof(int)));
+    JW_HIP_TRY(upload_async(dsmap, full.data(), full.size() * sizeof(int), s));
+  }
+  const PairMap pmf{dsmap, nfull, ns}, pm_all{nullptr, ns, ns};
   // forward FFTs read the padded signals in natural order (split N1n); the spectra are stored
-  // column-major for the inverse FFTs' split N1 x N/N1 (fft::split_n1)
+  // column-major for the inverse FFTs' split N1 x N/N1 (fft::split_n1), and in natural order
+  // for the band pass
   const long N1n = fft::split_n1(N, true), N1 = fft::split_n1(N, false);
   // forward FFT of the padded signals, gsig at a time
   for (long b0 = 0; b0 < batch && st == JW_OK; b0 += gsig) {
     const long nb = std::min<long>(gsig, batch - b0);
     PadIn in{x + b0 * n, n, N / N1n, padding};
-    st = run_fft<-1>(N, nb, in, SpecOut1{X, N, b0}, SpecOut{X, N, N1n, N1, N / N1, b0}, A, s, T,
-                     (ntm & 1) != 0);
+    const SpecOut so{X, N, N1n, N1, N / N1, b0};
+    if (Xn) {
+      st = run_fft<-1>(N, nb, in, SpecOut1{X, N, b0}, SpecOutBoth{so, Xn}, A, s, T, (ntm & 1) != 0);
+    } else {
+      st = run_fft<-1>(N, nb, in, SpecOut1{X, N, b0}, so, A, s, T, (ntm & 1) != 0);
+    }
   }
-  // per (signal, scale) pair: IFFT(X * psi_hat) -> coefficients
-  const long pairs = (long)batch * ns;
+  // band scales: one pass per (signal, scale) pair
+  if (nband > 0 && st == JW_OK) {
+    const dim3 gp((unsigned)((nb_hi * 512L + 255) / 256), (unsigned)nband);
+    if (wavelet == JW_CWT_MORLET) {
+      hipLaunchKernelGGL(cwt_band_psi<JW_CWT_MORLET>, gp, dim3(256), 0, s, dbands, psi, w, dsc,
+                         dsc + ns, N, N1b, fs);
+    } else {
+      hipLaunchKernelGGL(cwt_band_psi<JW_CWT_MEXHAT>, gp, dim3(256), 0, s, dbands, psi, w, dsc,
+                         dsc + ns, N, N1b, fs);
+    }
+    JW_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(cwt_band_roots, dim3((unsigned)((N1b + 255) / 256)), dim3(256), 0, s, wN1,
+                       N, N1b, T);
+    JW_HIP_TRY(hipGetLastError());
+    const CoefOut ob{out, n, N1b, 0, 1.0 / (double)N, (ntm & 2) != 0, pm_all};
+    const long items = (long)batch * nband;
+    const long blocks = (items + 7) / 8 * 8 * (N1b / fft::kT);
+    if (blocks > 0x7fffffffL) return fail(JW_ERR_UNSUPPORTED, "CWT band grid too large");
+    hipLaunchKernelGGL(cwt_band512, dim3((unsigned)blocks), dim3(512), 0, s, Xn, psi, dbands,
+                       nband, wN1, N, N1b, items, ob, T);
+    JW_HIP_TRY(hipGetLastError());
+  }
+  // the other (signal, scale) pairs: IFFT(X * psi_hat) -> coefficients in two passes
   if (pipe && st == JW_OK) {
     auto go = [&](auto kind) {
       constexpr int K = decltype(kind)::value;
       auto mk_in = [&](long p0) {
-        return ScaleIn<K>{X, dsc, w, N, N1, N / N1, p0, ns, fs, dsc + ns};
+        return ScaleIn<K>{X, dsc, w, N, N1, N / N1, p0, pmf, fs, dsc + ns};
       };
-      auto mk_out = [&](long p0) { return CoefOut{out, n, N1, p0, 1.0 / (double)N, (ntm & 2) != 0}; };
+      auto mk_out = [&](long p0) {
+        return CoefOut{out, n, N1, p0, 1.0 / (double)N, (ntm & 2) != 0, pmf};
+      };
       return fft::run_fft512_pipelined<1>(N, pairs, gpair, mk_in, mk_out, A, A + gpair * N, s, T,
                                           (ntm & 1) != 0);
     };
@@ -301,10 +572,10 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   }
   for (long p0 = 0; p0 < pairs && st == JW_OK && !pipe; p0 += gpair) {
     const long np_ = std::min<long>(gpair, pairs - p0);
-    CoefOut o{out, n, N <= 4096 ? 1 : N1, p0, 1.0 / (double)N, (ntm & 2) != 0};
-    CoefOut o1{out, n, 1, p0, 1.0 / (double)N, (ntm & 2) != 0};
+    CoefOut o{out, n, N <= 4096 ? 1 : N1, p0, 1.0 / (double)N, (ntm & 2) != 0, pmf};
+    CoefOut o1{out, n, 1, p0, 1.0 / (double)N, (ntm & 2) != 0, pmf};
     auto go = [&](auto kind) {
-      ScaleIn<decltype(kind)::value> in{X, dsc, w, N, N1, N <= 4096 ? 1 : N / N1, p0, ns, fs,
+      ScaleIn<decltype(kind)::value> in{X, dsc, w, N, N1, N <= 4096 ? 1 : N / N1, p0, pmf, fs,
                                         dsc + ns};
       return run_fft<1>(N, np_, in, o1, o, A, s, T, (ntm & 1) != 0);
     };

@@ -35,6 +35,10 @@ static_assert(kTile >= kT * fft::kXbuf, "tile must hold the exchange buffers");
 // lanes of every write group on one bank group (SQ_LDS_BANK_CONFLICT = 62 % of LDS cycles).
 __device__ __forceinline__ int out_slot(int n, int c) { return 8 * n + (c ^ ((n >> 3) & 7)); }
 
+template <int S, bool TWID, class Out>
+__device__ __forceinline__ void pass512_tail(cplx (&a)[8], const Out& out, long N, long N2,
+                                             const Tables& T, long item, long line0, cplx* tile);
+
 // IN_TILE: the line's inputs are strided (pass 1 over a natural-order array): stage 8 lines
 // through the tile.  TWID: apply the four-step twiddle W_N^(S n1 col) (pass 1).
 template <int S, bool IN_TILE, bool TWID, class In, class Out>
@@ -57,6 +61,16 @@ __device__ __forceinline__ void pass512_body(const In& in, const Out& out, long 
 #pragma unroll
     for (int r = 0; r < 8; ++r) a[r] = in(item, lane + 64 * r, line0 + c);
   }
+  pass512_tail<S, TWID>(a, out, N, N2, T, item, line0, tile);
+}
+
+// The rest of a 512-line pass once wave c holds line line0 + c as a[r] = x[lane + 64 r]: the
+// wavefront FFT, the four-step twiddle (TWID), and the 8-line output staged through the tile
+// (the tile must be free: callers barrier after their last read of it).
+template <int S, bool TWID, class Out>
+__device__ __forceinline__ void pass512_tail(cplx (&a)[8], const Out& out, long N, long N2,
+                                             const Tables& T, long item, long line0, cplx* tile) {
+  const int tid = threadIdx.x, lane = tid & 63, c = tid >> 6;
   fft::fft512_wave<S>(a, tile + c * fft::kXbuf, T.w512, lane);
   const int q = lane >> 3, k1 = lane & 7;
   if (TWID && N2 > 1) {
@@ -291,6 +305,14 @@ struct SpecOut {
   long item0;
   __device__ void operator()(long item, long idx, long line, cplx v) const {
     X[(item0 + item) * N + tpos(line + Nf * idx, N1, N2)] = v;
+  }
+};
+struct SpecOutBoth {  // SpecOut, and the same spectrum in natural order: Xn[item][k]
+  SpecOut a;
+  cplx* Xn;
+  __device__ void operator()(long item, long idx, long line, cplx v) const {
+    a(item, idx, line, v);
+    Xn[(a.item0 + item) * a.N + line + a.Nf * idx] = v;
   }
 };
 struct SpecOut1 {  // single pass: X[item][idx]

@@ -132,3 +132,24 @@ def test_sinusoid_peaks_at_matching_scale():
     r = CWT(MorletWavelet(*MORLET6)).transformFFT(x, scales, fs)
     best = scales[int(np.argmax(r.getScalogram()))]
     assert abs(MORLET6[1] / best - f0) / f0 < 0.08
+
+
+@pytest.mark.parametrize("kind", ["morlet", "mexhat"])
+@pytest.mark.parametrize("n", [1 << 13, 1 << 16, 1 << 18, 300001])
+def test_band_scales_one_pass(kind, n, monkeypatch):
+    # Scales whose psi_hat band spans few 512-bin blocks run the one-pass band kernel
+    # (cwt_band512); JW_CWT_BAND=0 sends every scale through the two-pass FFT.  The band drops
+    # only bins below e^-60 of psi_hat's peak, so both agree far inside the oracle tolerance.
+    scales = CWT.generateLogScales(2.0, 1024.0, 12)
+    wv, params = {"morlet": (MorletWavelet(*MORLET6), MORLET6),
+                  "mexhat": (MexicanHatWavelet(1.5), (1.5, 0.0))}[kind]
+    x = orc.fill_uniform(n, 5)
+    monkeypatch.setenv("JW_CWT_BAND", "1000")
+    band = CWT(wv).transformFFT(x, scales, 1.0).getCoefficients()
+    monkeypatch.setenv("JW_CWT_BAND", "0")
+    two = CWT(wv).transformFFT(x, scales, 1.0).getCoefficients()
+    assert nw(band, two) < 1e-13, nw(band, two)
+    ex = orc.cwt_fft(x, scales, 1.0, kind, params, 1, exact=True)
+    assert nw(band, ex) < TOL_EXACT
+    for i in range(len(scales)):  # per scale, against that scale's own magnitude
+        assert nw(band[i], ex[i]) < 1e-11, (i, nw(band[i], ex[i]))
