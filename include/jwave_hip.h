@@ -173,6 +173,19 @@ int jw_cwt_direct(int wavelet, const double* params, const double* x, long n,
                   const double* scales, int ns, double sampling_rate, int arith, double* out_reim,
                   int batch, int where, void* stream);
 
+/* CWTResult accessors over coefficient arrays (device-resident for JW_DEVICE), so a scalogram
+ * or magnitude map needs no copy of the complex coefficients to the host:
+ *   jw_cwt_magnitude: out[i] = |c_i| = sqrt(re^2 + im^2)  -- CWTResult.getMagnitude
+ *     (CWTResult.java:94-106, Complex.getMag :202-204), bit-identical to Java;
+ *   jw_cwt_phase: Complex.getPhi's quadrant rules in radians -- CWTResult.getPhase (:113-126);
+ *   jw_cwt_scalogram: energy[r] = sum_t |c[r][t]|^2 over rows of n coefficients --
+ *     CWTResult.getScalogram (:272-287), tree-summed (within 1e-15 relative of Java's loop).
+ * coef_reim: count (or rows x n) interleaved (re, im) values. */
+int jw_cwt_magnitude(const double* coef_reim, long count, double* out, int where, void* stream);
+int jw_cwt_phase(const double* coef_reim, long count, double* out, int where, void* stream);
+int jw_cwt_scalogram(const double* coef_reim, long rows, long n, double* energy, int where,
+                     void* stream);
+
 /* ======================================================================
  * Synthetic input (bench / tests): java.util.Random(seed0 + b).nextDouble()*2-1 for
  * signal b, generated in HBM with LCG jump-ahead.  Identical to the oracle's stream.

@@ -678,6 +678,42 @@ int jw_cwt_direct(int wavelet, const double* params, const double* x, long n,
              });
 }
 
+// CWTResult.getMagnitude / getPhase / getScalogram (CWTResult.java:94-126, :272-287)
+static int cwt_elementwise(const double* c, long count, double* out, int where, void* stream,
+                           int (*dev)(const double*, long, double*, hipStream_t)) {
+  clear_error();
+  if (count < 0) return fail(JW_ERR_ILLEGAL_ARGUMENT, "negative size (count=%ld)", count);
+  int st = check_where(where);
+  if (st != JW_OK) return st;
+  if (count == 0) return JW_OK;
+  if (!c || !out) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
+  return run(where, stream, c, (size_t)count * 2, out, (size_t)count,
+             [&](const double* ci, double* o, hipStream_t s) { return dev(ci, count, o, s); });
+}
+
+int jw_cwt_magnitude(const double* coef_reim, long count, double* out, int where, void* stream) {
+  return cwt_elementwise(coef_reim, count, out, where, stream, cwt_magnitude_device);
+}
+
+int jw_cwt_phase(const double* coef_reim, long count, double* out, int where, void* stream) {
+  return cwt_elementwise(coef_reim, count, out, where, stream, cwt_phase_device);
+}
+
+int jw_cwt_scalogram(const double* coef_reim, long rows, long n, double* energy, int where,
+                     void* stream) {
+  clear_error();
+  if (rows < 0 || n < 0)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "negative size (rows=%ld, n=%ld)", rows, n);
+  int st = check_where(where);
+  if (st != JW_OK) return st;
+  if (rows == 0) return JW_OK;
+  if (!coef_reim || !energy) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
+  return run(where, stream, coef_reim, (size_t)rows * n * 2, energy, (size_t)rows,
+             [&](const double* ci, double* o, hipStream_t s) {
+               return cwt_scalogram_device(ci, rows, n, o, s);
+             });
+}
+
 int jw_synth_uniform(double* x_dev, long n, int batch, long seed0, void* stream) {
   clear_error();
   if (n < 0 || batch < 0) return fail(JW_ERR_ILLEGAL_ARGUMENT, "negative size");

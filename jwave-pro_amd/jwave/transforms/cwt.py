@@ -24,8 +24,54 @@ class PaddingType(enum.IntEnum):  # ContinuousWaveletTransform.java:74-79
     CONSTANT = _native.JW_PAD_CONSTANT
 
 
+def _reim(c):
+    """(Arr over the interleaved (re, im) doubles of complex coefficients, leading shape)."""
+    from .._arrays import Arr, _is_torch
+    if _is_torch(c):
+        import torch
+        if c.device.type == "cuda":
+            return Arr(torch.view_as_real(c.detach().to(torch.complex128).contiguous()), True), \
+                tuple(c.shape)
+        c = c.detach().cpu().numpy()
+    a = np.ascontiguousarray(np.asarray(c, dtype=np.complex128))
+    return Arr(a.view(np.float64), False), a.shape
+
+
+def magnitude(coefficients):
+    """CWTResult.getMagnitude on the engine (jw_cwt_magnitude): |c| for any shape of complex
+    coefficients -- a HIP-device torch tensor stays on the device (JW_DEVICE)."""
+    x, shape = _reim(coefficients)
+    out = x.empty(shape)
+    _native.check(_native.lib().jw_cwt_magnitude(x.ptr, int(np.prod(shape)), out.ptr, x.where,
+                                                 x.stream))
+    return out.obj
+
+
+def phase(coefficients):
+    """CWTResult.getPhase on the engine (jw_cwt_phase): Complex.getPhi in radians."""
+    x, shape = _reim(coefficients)
+    out = x.empty(shape)
+    _native.check(_native.lib().jw_cwt_phase(x.ptr, int(np.prod(shape)), out.ptr, x.where,
+                                             x.stream))
+    return out.obj
+
+
+def scalogram(coefficients):
+    """CWTResult.getScalogram on the engine (jw_cwt_scalogram): sum over the last axis of |c|^2
+    (ns x n -> ns; B x ns x n -> B x ns)."""
+    x, shape = _reim(coefficients)
+    n = shape[-1] if shape else 1
+    rows = int(np.prod(shape[:-1])) if len(shape) > 1 else 1
+    out = x.empty(shape[:-1] if len(shape) > 1 else (1,))
+    _native.check(_native.lib().jw_cwt_scalogram(x.ptr, rows, n, out.ptr, x.where, x.stream))
+    return out.obj
+
+
 class CWTResult:
-    """jwave.transforms.CWTResult (CWTResult.java:33-287); coefficients as complex128."""
+    """jwave.transforms.CWTResult (CWTResult.java:33-287); coefficients as complex128.
+
+    Coefficients held as a HIP-device torch tensor (``ContinuousWaveletTransform.resultOf``)
+    keep getMagnitude / getPhase / getScalogram on the device (magnitude, phase, scalogram)."""
 
     def __init__(self, coefficients, scales, timeAxis, samplingRate, waveletName):
         self._c = coefficients
@@ -37,10 +83,17 @@ class CWTResult:
     def getCoefficients(self):
         return self._c
 
+    def _on_device(self):
+        return type(self._c).__module__.startswith("torch")
+
     def getMagnitude(self):  # Complex.getMag :202-204
+        if self._on_device():
+            return magnitude(self._c)
         return np.sqrt(self._c.real * self._c.real + self._c.imag * self._c.imag)
 
     def getPhase(self):  # Complex.getPhi :213-226 (degrees, quadrant rules) -> radians
+        if self._on_device():
+            return phase(self._c)
         r, j = self._c.real, self._c.imag
         with np.errstate(divide="ignore", invalid="ignore"):
             phi = np.degrees(np.arctan(np.abs(j / r)))
@@ -50,10 +103,12 @@ class CWTResult:
         return out * math.pi / 180.0
 
     def getReal(self):
-        return self._c.real.copy()
+        r = self._c.real
+        return r.clone() if self._on_device() else r.copy()
 
     def getImaginary(self):
-        return self._c.imag.copy()
+        r = self._c.imag
+        return r.clone() if self._on_device() else r.copy()
 
     def getScales(self):
         return self._scales
@@ -72,7 +127,8 @@ class CWTResult:
     def getCoefficientsAtTime(self, timeIndex):
         if timeIndex < 0 or timeIndex >= self._c.shape[1]:
             raise IndexError("Time index out of bounds")
-        return self._c[:, timeIndex].copy()
+        r = self._c[:, timeIndex]
+        return r.clone() if self._on_device() else r.copy()
 
     def getSamplingRate(self):
         return self._fs
@@ -87,6 +143,8 @@ class CWTResult:
         return len(self._time)
 
     def getScalogram(self):  # sum_t |c|^2 per scale (CWTResult.java:272-287)
+        if self._on_device():
+            return scalogram(self._c)
         m = self.getMagnitude()
         return np.array([float(np.sum(row * row)) for row in m])
 
@@ -153,6 +211,14 @@ class ContinuousWaveletTransform:
         return CWTResult(coeffs, scales, time_axis, samplingRate, self._wavelet.getName())
 
     transformFFTParallel = transformFFT  # same values (ContinuousWaveletTransform.java:511-565)
+
+    def resultOf(self, coefficients, scales, samplingRate=1.0):
+        """A CWTResult over ns x n coefficients as they are (e.g. one signal of a device-resident
+        transformFFTBatch): its accessors then run on the engine without a host copy."""
+        n = coefficients.shape[-1]
+        dt = 1.0 / samplingRate
+        time_axis = np.array([i * dt for i in range(n)])  # createTimeAxis
+        return CWTResult(coefficients, scales, time_axis, samplingRate, self._wavelet.getName())
 
     # ---- direct (time-domain) path: transform :141-172, computeCoefficient :240-260 ----
     def _run_direct(self, x, scales, samplingRate, arith):

@@ -314,3 +314,19 @@ def test_wpt_validation_messages():
         t.forward(np.ones(8), 4)
     with pytest.raises(JWaveFailure, match="WaveletPacketTransform#reverse - given level is out"):
         t.reverse(np.ones(8), -1)
+
+
+def test_cwt_result_abi_validation():
+    # jw_cwt_magnitude / jw_cwt_phase / jw_cwt_scalogram: argument checks before any HIP call
+    L = _native.lib()
+    x = np.zeros(8)
+    out = np.zeros(4)
+    p = x.ctypes.data_as(ctypes.c_void_p)
+    o = out.ctypes.data_as(ctypes.c_void_p)
+    assert L.jw_cwt_magnitude(p, -1, o, 0, None) == -1
+    assert L.jw_cwt_phase(p, 4, o, 5, None) == -1
+    assert L.jw_cwt_scalogram(p, -1, 4, o, 0, None) == -1
+    assert L.jw_cwt_scalogram(p, 1, -4, o, 0, None) == -1
+    assert L.jw_cwt_magnitude(p, 0, o, 0, None) == 0
+    assert L.jw_cwt_scalogram(p, 0, 4, o, 1, None) == 0
+    assert L.jw_cwt_magnitude(None, 4, o, 0, None) == -1

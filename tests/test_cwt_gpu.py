@@ -153,3 +153,39 @@ def test_band_scales_one_pass(kind, n, monkeypatch):
     assert nw(band, ex) < TOL_EXACT
     for i in range(len(scales)):  # per scale, against that scale's own magnitude
         assert nw(band[i], ex[i]) < 1e-11, (i, nw(band[i], ex[i]))
+
+
+def test_result_accessors_on_device(device):
+    # CWTResult.getMagnitude / getPhase / getScalogram (CWTResult.java:94-126, :272-287) on
+    # device coefficients (jw_cwt_magnitude / _phase / _scalogram): no host copy of the
+    # scalogram's input.  Magnitude bit-identical to Complex.getMag's sqrt(re^2 + im^2).
+    import torch
+    from jwave.transforms import cwt
+    n, B = 1 << 14, 2
+    scales = CWT.generateLogScales(2.0, 256.0, 9)
+    xs = np.stack([orc.fill_uniform(n, 31 + b) for b in range(B)])
+    t = CWT(MorletWavelet(*MORLET6))
+    dev = t.transformFFTBatch(torch.from_numpy(xs).to(device), scales)
+    host = dev.cpu().numpy()
+    r = t.resultOf(dev[1], scales)
+    hr = t.resultOf(host[1], scales)
+    mag = r.getMagnitude()
+    assert mag.is_cuda and mag.shape == (9, n)
+    assert np.array_equal(mag.cpu().numpy(), hr.getMagnitude())
+    assert np.max(np.abs(r.getPhase().cpu().numpy() - hr.getPhase())) < 1e-13
+    sg = r.getScalogram().cpu().numpy()
+    assert np.max(np.abs(sg - hr.getScalogram()) / hr.getScalogram()) < 1e-13
+    sgb = cwt.scalogram(dev).cpu().numpy()  # B x ns in one launch
+    assert sgb.shape == (B, 9) and np.allclose(sgb[1], sg, rtol=1e-15, atol=0)
+    hm = cwt.magnitude(host)  # JW_HOST staging path
+    assert np.array_equal(hm, np.sqrt(host.real * host.real + host.imag * host.imag))
+    # quadrant edge cases of Complex.getPhi
+    c = np.array([1 + 1j, -1 + 0j, 0j, -2 - 2j, 1 - 1j, -0.0 + 3j, 0.0 - 3j])
+    ph = cwt.phase(torch.from_numpy(c).to(device)).cpu().numpy()
+    ref = CWTResult_host_phase(c)
+    assert np.max(np.abs(ph - ref)) < 1e-15
+
+
+def CWTResult_host_phase(c):
+    from jwave.transforms import CWTResult
+    return CWTResult(c.reshape(1, -1), [1.0], np.arange(c.size), 1.0, "x").getPhase()[0]
