@@ -185,6 +185,13 @@ int jw_cwt_magnitude(const double* coef_reim, long count, double* out, int where
 int jw_cwt_phase(const double* coef_reim, long count, double* out, int where, void* stream);
 int jw_cwt_scalogram(const double* coef_reim, long rows, long n, double* energy, int where,
                      void* stream);
+/* ContinuousWaveletTransform.transformFFT(x_b, scales, fs).getScalogram() for batch signals
+ * (ContinuousWaveletTransform.java:183-229 then CWTResult.java:272-287) with the coefficients
+ * kept on the GPU (signals in chunks of <= ~2 GiB of coefficients): energy is batch x ns.
+ * Argument checks and messages as jw_cwt_fft. */
+int jw_cwt_fft_scalogram(int wavelet, const double* params, const double* x, long n,
+                         const double* scales, int ns, double sampling_rate, int padding,
+                         double* energy, int batch, int where, void* stream);
 
 /* ======================================================================
  * Synthetic input (bench / tests): java.util.Random(seed0 + b).nextDouble()*2-1 for

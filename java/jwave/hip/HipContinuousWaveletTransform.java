@@ -79,6 +79,16 @@ public class HipContinuousWaveletTransform extends ContinuousWaveletTransform {
     return result(rows, scales, signal.length, samplingRate);
   }
 
+  /**
+   * transformFFT(signal, scales, samplingRate).getScalogram() (CWTResult.java:272-287) with the
+   * ns x n coefficients kept on the GPU: only the ns energies cross PCIe.
+   */
+  public double[] transformFFTScalogram(double[] signal, double[] scales, double samplingRate) {
+    int k = kind();
+    if (k < 0) return super.transformFFT(signal, scales, samplingRate).getScalogram();
+    return nScalogramFFT(k, params(), signal, scales, samplingRate, padding);
+  }
+
   @Override
   public CWTResult transformFFTParallel(double[] signal, double[] scales, double samplingRate) {
     return transformFFT(signal, scales, samplingRate); // same values (:511-565)
@@ -99,6 +109,8 @@ public class HipContinuousWaveletTransform extends ContinuousWaveletTransform {
 
   private static native double[][] nTransformFFT(int kind, double[] params, double[] x,
                                                  double[] scales, double fs, int padding);
+  private static native double[] nScalogramFFT(int kind, double[] params, double[] x,
+                                               double[] scales, double fs, int padding);
   private static native double[][] nTransformDirect(int kind, double[] params, double[] x,
                                                     double[] scales, double fs, int arith);
 }

@@ -313,6 +313,34 @@ JNIEXPORT jobjectArray JNICALL Java_jwave_hip_HipContinuousWaveletTransform_nTra
   return rows;
 }
 
+/* transformFFT(...).getScalogram() without the coefficients crossing PCIe: double[ns] */
+JNIEXPORT jdoubleArray JNICALL Java_jwave_hip_HipContinuousWaveletTransform_nScalogramFFT(
+    JNIEnv* env, jclass cls, jint kind, jdoubleArray params, jdoubleArray x, jdoubleArray scales,
+    jdouble fs, jint padding) {
+  (void)cls;
+  jsize n = 0, ns = 0;
+  double* pr = copy_in(env, params, NULL);
+  double* xs = pr ? copy_in(env, x, &n) : NULL;
+  double* sc = xs ? copy_in(env, scales, &ns) : NULL;
+  double* e = sc ? malloc(sizeof(double) * (size_t)(ns ? ns : 1)) : NULL;
+  if (!e) {
+    if (sc) oom(env);
+    free(pr), free(xs), free(sc);
+    return NULL;
+  }
+  const int st =
+      jw_cwt_fft_scalogram(kind, pr, xs, (long)n, sc, ns, fs, padding, e, 1, JW_HOST, NULL);
+  free(pr), free(xs), free(sc);
+  jdoubleArray out = NULL;
+  if (st == JW_OK) {
+    out = (*env)->NewDoubleArray(env, ns);
+    if (out) (*env)->SetDoubleArrayRegion(env, out, 0, ns, e);
+  }
+  free(e);
+  if (st != JW_OK) jw_throw(env, st);
+  return out;
+}
+
 /* the direct (time-domain) CWT, same shapes; arith: JW_ARITH_* */
 JNIEXPORT jobjectArray JNICALL Java_jwave_hip_HipContinuousWaveletTransform_nTransformDirect(
     JNIEnv* env, jclass cls, jint kind, jdoubleArray params, jdoubleArray x, jdoubleArray scales,

@@ -621,10 +621,9 @@ static int cwt_wavelet_check(int wavelet, const double* params) {
   return JW_OK;
 }
 
-int jw_cwt_fft(int wavelet, const double* params, const double* x, long n, const double* scales,
-               int ns, double sampling_rate, int padding, double* out_reim, int batch, int where,
-               void* stream) {
-  clear_error();
+// jw_cwt_fft's argument checks (shared with jw_cwt_fft_scalogram)
+static int cwt_fft_check(int wavelet, const double* params, long n, const double* scales, int ns,
+                         int padding, int batch, int where) {
   if (int st = cwt_wavelet_check(wavelet, params); st != JW_OK) return st;
   if (n < 0 || ns < 0 || batch < 0)
     return fail(JW_ERR_ILLEGAL_ARGUMENT, "negative size (n=%ld, ns=%d, batch=%d)", n, ns, batch);
@@ -634,7 +633,14 @@ int jw_cwt_fft(int wavelet, const double* params, const double* x, long n, const
   // ContinuousWavelet.fourierTransform :123-125 (PaulWavelet's override :152-164 has no check)
   for (int i = 0; i < ns && n > 0 && wavelet != JW_CWT_PAUL; ++i)
     if (!(scales[i] > 0)) return fail(JW_ERR_ILLEGAL_ARGUMENT, "Scale must be positive");
-  int st = check_where(where);
+  return check_where(where);
+}
+
+int jw_cwt_fft(int wavelet, const double* params, const double* x, long n, const double* scales,
+               int ns, double sampling_rate, int padding, double* out_reim, int batch, int where,
+               void* stream) {
+  clear_error();
+  int st = cwt_fft_check(wavelet, params, n, scales, ns, padding, batch, where);
   if (st != JW_OK) return st;
   if (n == 0 || ns == 0 || batch == 0) return JW_OK;
   const size_t nin = (size_t)batch * n, nout = (size_t)batch * ns * n * 2;
@@ -642,6 +648,38 @@ int jw_cwt_fft(int wavelet, const double* params, const double* x, long n, const
              [&](const double* xi, double* o, hipStream_t s) {
                return cwt_fft_device(wavelet, params, xi, n, scales, ns, sampling_rate, padding,
                                      o, batch, s);
+             });
+}
+
+// transformFFT(...).getScalogram() with the coefficients kept in a device workspace (signals
+// in chunks of at most ~2 GiB of coefficients): only batch x ns energies leave the GPU.
+int jw_cwt_fft_scalogram(int wavelet, const double* params, const double* x, long n,
+                         const double* scales, int ns, double sampling_rate, int padding,
+                         double* energy, int batch, int where, void* stream) {
+  clear_error();
+  int st = cwt_fft_check(wavelet, params, n, scales, ns, padding, batch, where);
+  if (st != JW_OK) return st;
+  if (ns == 0 || batch == 0) return JW_OK;
+  const size_t nin = (size_t)batch * n, nout = (size_t)batch * ns;
+  return run(where, stream, x, nin, energy, nout,
+             [&](const double* xi, double* o, hipStream_t s) {
+               if (n == 0) {  // no time points: zero energy (CWTResult.java:277-284)
+                 JW_HIP_TRY(hipMemsetAsync(o, 0, nout * sizeof(double), s));
+                 return (int)JW_OK;
+               }
+               const long per_sig = (long)ns * n * 2 * (long)sizeof(double);
+               const long chunk = std::max(1L, std::min<long>(batch, (2L << 30) / per_sig));
+               StreamAllocs mem(s);
+               double* coef = nullptr;
+               JW_HIP_TRY(mem.alloc(&coef, (size_t)chunk * per_sig));
+               for (long b0 = 0; b0 < batch; b0 += chunk) {
+                 const int nb = (int)std::min<long>(chunk, batch - b0);
+                 int r = cwt_fft_device(wavelet, params, xi + b0 * n, n, scales, ns,
+                                        sampling_rate, padding, coef, nb, s);
+                 if (r == JW_OK) r = cwt_scalogram_device(coef, (long)nb * ns, n, o + b0 * ns, s);
+                 if (r != JW_OK) return r;
+               }
+               return (int)JW_OK;
              });
 }
 

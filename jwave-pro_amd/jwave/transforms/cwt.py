@@ -212,6 +212,23 @@ class ContinuousWaveletTransform:
 
     transformFFTParallel = transformFFT  # same values (ContinuousWaveletTransform.java:511-565)
 
+    def transformFFTScalogram(self, signals, scales, samplingRate=1.0):
+        """transformFFT(x, scales, fs).getScalogram() for one signal (-> ns) or B x n signals
+        (-> B x ns), numpy or HIP-device torch; the coefficients never leave the GPU
+        (jw_cwt_fft_scalogram)."""
+        x = as_input(signals)
+        one = len(x.shape) == 1
+        if one:
+            x = as_input(x.obj.reshape(1, -1))
+        sc = np.ascontiguousarray(np.asarray(scales, dtype=np.float64).ravel())
+        B, n = x.shape
+        out = x.empty((B, sc.shape[0]))
+        params = (ctypes.c_double * 2)(*self._wavelet.params())
+        _native.check(_native.lib().jw_cwt_fft_scalogram(
+            self._wavelet._kind, params, x.ptr, n, sc.ctypes.data_as(ctypes.c_void_p), sc.shape[0],
+            float(samplingRate), int(self._paddingType), out.ptr, B, x.where, x.stream))
+        return out.obj[0] if one else out.obj
+
     def resultOf(self, coefficients, scales, samplingRate=1.0):
         """A CWTResult over ns x n coefficients as they are (e.g. one signal of a device-resident
         transformFFTBatch): its accessors then run on the engine without a host copy."""

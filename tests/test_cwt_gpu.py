@@ -189,3 +189,22 @@ def test_result_accessors_on_device(device):
 def CWTResult_host_phase(c):
     from jwave.transforms import CWTResult
     return CWTResult(c.reshape(1, -1), [1.0], np.arange(c.size), 1.0, "x").getPhase()[0]
+
+
+def test_fft_scalogram_fused(device):
+    # jw_cwt_fft_scalogram: transformFFT(...).getScalogram() with the coefficients kept in HBM
+    import torch
+    n, B = 5000, 3
+    scales = CWT.generateLogScales(1.0, 300.0, 11)
+    xs = np.stack([orc.fill_uniform(n, 41 + b) for b in range(B)])
+    t = CWT(MorletWavelet(*MORLET6))
+    e = t.transformFFTScalogram(xs, scales)
+    assert e.shape == (B, 11)
+    for b in range(B):
+        ref = t.transformFFT(xs[b], scales).getScalogram()
+        assert np.max(np.abs(e[b] - ref) / ref) < 1e-13
+    e1 = t.transformFFTScalogram(xs[1], scales)
+    assert np.array_equal(e1, e[1])
+    ed = t.transformFFTScalogram(torch.from_numpy(xs).to(device), scales)
+    assert ed.is_cuda and np.array_equal(ed.cpu().numpy(), e)
+    assert np.array_equal(t.transformFFTScalogram(np.zeros((2, 0)), scales), np.zeros((2, 11)))
