@@ -288,17 +288,21 @@ __global__ __launch_bounds__(512) void cwt_band512(const cplx* __restrict__ Xn,
                                                    const double* __restrict__ psi,
                                                    const BandScale* __restrict__ bands, int nband,
                                                    const double4* __restrict__ wN1, long N, long N1,
-                                                   long items, CoefOut out, Tables T) {
+                                                   long items, CoefOut out, Tables T, int R) {
   __shared__ cplx tile[fft::kTile];
   // 32-bit index math (the scalar unit runs 64-bit division as a ~100-instruction sequence)
-  const unsigned lrpp = (unsigned)__builtin_ctzl(N1 / fft::kT), local = blockIdx.x >> 3;
+  const unsigned lrpp = (unsigned)__builtin_ctzl(N1 / (fft::kT * R)), local = blockIdx.x >> 3;
   const unsigned slot = local >> lrpp;
   const unsigned item = slot * 8 + (blockIdx.x & 7);
   const unsigned rg = local - (slot << lrpp);
   if (item >= (unsigned long)items) return;
-  const long r0 = (long)rg * fft::kT;
   const unsigned sig = item / (unsigned)nband;
   const BandScale b = bands[item - sig * (unsigned)nband];
+  // R row groups per workgroup, one after the other: the output stores of one group drain
+  // while the band sums of the next run
+  for (int it = 0; it < R; ++it) {
+  const long r0 = ((long)rg * R + it) * fft::kT;
+  __syncthreads();  // the previous group's staging reads are done with the tile
   // thread (h, kp): columns kp and kp + 256, rows r0 + 4h .. r0 + 4h + 3 (h uniform per wave,
   // so each wave-uniform twiddle feeds two columns)
   const int tid = threadIdx.x, lane = tid & 63, c = tid >> 6, h = tid >> 8, kp = tid & 255;
@@ -371,6 +375,7 @@ __global__ __launch_bounds__(512) void cwt_band512(const cplx* __restrict__ Xn,
   CoefOut o = out;
   o.pair0 = (long)sig * out.pm.ns + b.s;  // one output pair per workgroup
   fft::pass512_tail<1, false>(a, o, N, 512L, T, 0L, r0, tile);
+  }
 }
 
 }  // namespace
@@ -543,10 +548,14 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     JW_HIP_TRY(hipGetLastError());
     const CoefOut ob{out, n, N1b, 0, 1.0 / (double)N, (ntm & 2) != 0, pm_all};
     const long items = (long)batch * nband;
-    const long blocks = (items + 7) / 8 * 8 * (N1b / fft::kT);
+    const char* grr = std::getenv("JW_CWT_BAND_R");  // A/B runs: row groups per workgroup
+    int R = grr ? std::atoi(grr) : 8;  // measured: 1 -> 44.6, 4 -> 42.5, 8 -> 41.7 ms at cfg3
+    while (R > 1 && (N1b / fft::kT) % R) R >>= 1;
+    R = std::max(1, std::min<int>(R, (int)(N1b / fft::kT)));
+    const long blocks = (items + 7) / 8 * 8 * (N1b / fft::kT / R);
     if (blocks > 0x7fffffffL) return fail(JW_ERR_UNSUPPORTED, "CWT band grid too large");
     hipLaunchKernelGGL(cwt_band512, dim3((unsigned)blocks), dim3(512), 0, s, Xn, psi, dbands,
-                       nband, wN1, N, N1b, items, ob, T);
+                       nband, wN1, N, N1b, items, ob, T, R);
     JW_HIP_TRY(hipGetLastError());
   }
   // the other (signal, scale) pairs: IFFT(X * psi_hat) -> coefficients in two passes
