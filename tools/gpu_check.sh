@@ -1,5 +1,7 @@
 #!/bin/bash
-# One GPU session: parity tests, then (only if no crash) the bench and a rocprofv3 kernel trace.
+# One GPU session: parity tests, then (only if no crash) the bench and a rocprofv3 kernel trace
+# of the headline launches only (--no-check --no-alt --no-cpu-baseline: no host-path, AUTO or
+# STRICT legs, so each kernel's average in the stats is the timed launch's duration).
 # Every GPU step has its own time limit; a crash/timeout ends the script.
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R" || exit 2
@@ -15,7 +17,7 @@ echo "bench rc=$rc"; tail -3 gpurun_out/bench_$TAG.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$TAG" -o run --output-format csv \
-  -- python3 "$R/bench.py" > "$R/gpurun_out/prof_$TAG.log" 2>&1
+  -- python3 "$R/bench.py" --no-check --no-alt --no-cpu-baseline > "$R/gpurun_out/prof_$TAG.log" 2>&1
 rc=$?
 echo "rocprof rc=$rc"; tail -2 "$R/gpurun_out/prof_$TAG.log"
 exit $rc
