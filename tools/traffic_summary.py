@@ -10,7 +10,7 @@ import sys
 
 d = sys.argv[1]
 out = {}
-STEP_KERNELS = {"cwt": ("pass512",), "fwt2d": ("fwt_",)}
+STEP_KERNELS = {"cwt": ("pass512", "cwt_band"), "fwt2d": ("fwt_",)}
 for w, keys in STEP_KERNELS.items():
     tot = {}
     per_kernel = collections.defaultdict(float)
