@@ -305,20 +305,24 @@ __device__ __forceinline__ void cascade_rev(double* buf, int n, int h0, int tw, 
     // are all thread tid = u of the first pass (nslow <= 32)
     const int nslow = h < M ? half : (M >> 1) - 1 < half ? (M >> 1) - 1 : half;
     d2 o[P];
-    // The wave holding the wrapped pairs (u < nslow, all in the first 64 threads' first
-    // pass) runs that pass in the rotated order for all its lanes -- one pass with LDS taps
-    // instead of the plain pass plus a second one for 7 lanes, which held every barrier.
-    const bool rot_wave = h >= M && NTL >= 64 && (tid >> 6) == 0;
+    // STRICT: the wave holding the wrapped pairs (u < nslow, all in the first 64 threads'
+    // first pass) runs that pass in the rotated order for all its lanes -- one pass with LDS
+    // taps instead of the plain pass plus a second one for 7 lanes, which held every barrier.
+    // FMA (a tolerance contract, the order is free): every pair, wrapped or not, takes the
+    // plain descending tap order with its index taken mod h/2, so no lane is special.
+    const bool fma_wrap = FMA && h >= M;
+    const bool rot_wave = !fma_wrap && h >= M && NTL >= 64 && (tid >> 6) == 0;
 #pragma unroll
     for (int r = 0; r < P; ++r) {
       const int u = tid + r * NTL;
       if (r == 0 && rot_wave) {
         if (u < half) o[0] = rev_pair_rot<FMA, M, KIND>(buf, h, u, tp);
-      } else if (u < half && u >= nslow) {
+      } else if (u < half && (fma_wrap || u >= nslow)) {
         double a0 = 0., a1 = 0.;
 #pragma unroll
         for (int t = (M >> 1) - 1; t >= 0; --t) {
-          const double av = buf[u - t], dv = buf[u - t + half];
+          const int i = fma_wrap ? (u - t) & (half - 1) : u - t;
+          const double av = buf[i], dv = buf[i + half];
           a0 = rev_acc<FMA, KIND>(a0, av, dv, f.sR[2 * t], f.wR[2 * t]);  // KIND: compile-time
           a1 = rev_acc<FMA, KIND>(a1, av, dv, f.sR[2 * t + 1], f.wR[2 * t + 1]);
         }
@@ -326,7 +330,7 @@ __device__ __forceinline__ void cascade_rev(double* buf, int n, int h0, int tw, 
       }
       if (u + NTL >= half) break;
     }
-    if (tid < nslow && !rot_wave)
+    if (tid < nslow && !rot_wave && !fma_wrap)
       o[0] = h >= M ? rev_pair_rot<FMA, M, KIND>(buf, h, tid, tp)
                     : rev_pair_wrapped<FMA, M, KIND>(buf, h, tid, f);
     if (gout && h == n) {
