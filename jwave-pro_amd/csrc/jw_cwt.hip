@@ -284,6 +284,9 @@ __global__ __launch_bounds__(256) void cwt_band_roots(double4* w, long N, long N
 // W_N1^(k1 n1) are uniform over the workgroup: scalar loads from the N1-entry root table.
 // Placement: the rpp = N1/8 workgroups of a pair share blockIdx % 8 (one XCD under the
 // round-robin dispatch), so the pair's band of X is fetched into one L2, not eight (speed only).
+typedef double d4v __attribute__((ext_vector_type(4)));
+
+template <bool MF>
 __global__ __launch_bounds__(512) void cwt_band512(const cplx* __restrict__ Xn,
                                                    const double* __restrict__ psi,
                                                    const BandScale* __restrict__ bands, int nband,
@@ -300,13 +303,15 @@ __global__ __launch_bounds__(512) void cwt_band512(const cplx* __restrict__ Xn,
   const BandScale b = bands[item - sig * (unsigned)nband];
   // R row groups per workgroup, one after the other: the output stores of one group drain
   // while the band sums of the next run
+  const int tid = threadIdx.x, lane = tid & 63, c = tid >> 6;
   for (int it = 0; it < R; ++it) {
   const long r0 = ((long)rg * R + it) * fft::kT;
   __syncthreads();  // the previous group's staging reads are done with the tile
   // thread (h, kp): columns kp and kp + 256, rows r0 + 4h .. r0 + 4h + 3 (h uniform per wave,
   // so each wave-uniform twiddle feeds two columns)
-  const int tid = threadIdx.x, lane = tid & 63, c = tid >> 6, h = tid >> 8, kp = tid & 255;
   const unsigned m1 = (unsigned)N1 - 1;
+  if constexpr (!MF) {
+  const int h = tid >> 8, kp = tid & 255;
   const unsigned rr = __builtin_amdgcn_readfirstlane((unsigned)r0 + 4 * h);  // wave-uniform
   // sum_j z w as three real sums (Gauss): s1 = sum zr c, s2 = sum zi d, s3 = sum (zr+zi)(c+d);
   // re = s1 - s2, im = s3 - s1 - s2: three multiply-adds per term instead of four
@@ -366,6 +371,58 @@ __global__ __launch_bounds__(512) void cwt_band512(const cplx* __restrict__ Xn,
     tile[(4 * h + t) * 512 + kp] = fft::cmul(v0, w0);
     tile[(4 * h + t) * 512 + kp + 256] = fft::cmul(v1, fft::cmul(w0, u));
     if (t < 3) w0 = fft::cmul(w0, st);
+  }
+  } else {
+  // The same sums as a real GEMM on the matrix cores (v_mfma_f64_16x16x4_f64): rows 0..7 are
+  // Re A[r0 + t][.], rows 8..15 Im A[r0 + t][.]; K runs over (block j, re/im of Z_j):
+  //   [Re; Im] A = [[Re W, -Im W], [Im W, Re W]] [Re Z; Im Z],   W_tj = W_N1^(k1_j (r0 + t)).
+  // Wave c owns columns 64c .. 64c + 63 (four 16-column tiles); one MFMA per tile consumes two
+  // blocks.  Lane l holds A[l & 15][k = l >> 4] and B[k = l >> 4][col l & 15] (the f32
+  // 16x16x4 operand maps), and D[row (l >> 4) + 4 r][col l & 15] (the f64 C/D map).
+  const int tr = lane & 15, kq = lane >> 4;  // A row / B column, K index
+  const int t = tr & 7, im_row = tr >> 3, jo = kq >> 1, zc = kq & 1;
+  d4v acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = d4v{0.0, 0.0, 0.0, 0.0};
+  // each lane loads only the part of Z it feeds (re for kq even, im for kq odd): 8-byte loads
+  const double* xs = (const double*)(Xn + (long)sig * N + 64 * c + tr) + zc;
+  const double* ps = psi + b.psi_off + 64 * c + tr;
+  for (int j0 = 0; j0 < b.nb; j0 += 2) {
+    const int j = j0 + jo;
+    const bool in = j < b.nb;
+    const int jj = in ? j : b.nb - 1;
+    const unsigned k1 = ((unsigned)b.b0 + jj) & m1;
+    const double4 w = wN1[(k1 * ((unsigned)r0 + t)) & m1];
+    // A[tr][kq]: Re row: (Re W, -Im W) for (Re Z, Im Z); Im row: (Im W, Re W)
+    double av = im_row ? (zc ? w.x : w.y) : (zc ? -w.y : w.x);
+    av = in ? av : 0.0;
+    double xv[4], pv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      xv[q] = xs[2 * (512L * k1 + 16 * q)];
+      pv[q] = ps[512 * jj + 16 * q];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const double bv = xv[q] * pv[q];
+      acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[q], 0, 0, 0);
+    }
+  }
+  // lane: D rows (l >> 4) + 4 r -> Re of rows t0, t0 + 4 (r = 0, 1), Im of them (r = 2, 3);
+  // four-step twiddle W_N^(n1 col), col = 64 c + 16 q + tr, by a step of 16 columns per tile
+  const int t0 = lane >> 4;
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const long n1 = r0 + t0 + 4 * e, col0 = 64 * c + tr;
+    cplx w0 = fft::twiddle(T, (n1 * col0) & (N - 1));
+    const cplx st = fft::twiddle(T, (16 * n1) & (N - 1));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const cplx v = make_double2(acc[q][e], acc[q][e + 2]);
+      tile[(t0 + 4 * e) * 512 + col0 + 16 * q] = fft::cmul(v, w0);
+      if (q < 3) w0 = fft::cmul(w0, st);
+    }
+  }
   }
   __syncthreads();
   cplx a[8];
@@ -554,8 +611,14 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     R = std::max(1, std::min<int>(R, (int)(N1b / fft::kT)));
     const long blocks = (items + 7) / 8 * 8 * (N1b / fft::kT / R);
     if (blocks > 0x7fffffffL) return fail(JW_ERR_UNSUPPORTED, "CWT band grid too large");
-    hipLaunchKernelGGL(cwt_band512, dim3((unsigned)blocks), dim3(512), 0, s, Xn, psi, dbands,
-                       nband, wN1, N, N1b, items, ob, T, R);
+    const char* gmf = std::getenv("JW_CWT_BAND_MFMA");  // A/B runs: 0 = VALU band sums
+    if (gmf && gmf[0] == '0') {
+      hipLaunchKernelGGL(cwt_band512<false>, dim3((unsigned)blocks), dim3(512), 0, s, Xn, psi,
+                         dbands, nband, wN1, N, N1b, items, ob, T, R);
+    } else {
+      hipLaunchKernelGGL(cwt_band512<true>, dim3((unsigned)blocks), dim3(512), 0, s, Xn, psi,
+                         dbands, nband, wN1, N, N1b, items, ob, T, R);
+    }
     JW_HIP_TRY(hipGetLastError());
   }
   // the other (signal, scale) pairs: IFFT(X * psi_hat) -> coefficients in two passes
