@@ -377,6 +377,181 @@ __global__ __launch_bounds__(kNT2) void fwt_rev_lds2(const double* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------------
+// 4096-sample rows (the cfg4 2-D row pass, and 1-D signals of that length): the cascades
+// above with every level size a compile-time constant (the levels are unrolled), so each
+// thread's LDS reads come off one base address with immediate offsets -- the mask and shift
+// per tap pair of the runtime-h loops was ~40 % of their VALU instructions.
+//  * forward: the circular wrap (2i + j) mod h is a copy of the level's first M - 2 inputs
+//    after its end (buf[h .. h + M - 2)), written by the level before; the details of every
+//    level go from registers straight to global memory (they are final), only the
+//    approximations return to LDS.
+//  * reverse: the wrapped pairs (u < M/2 - 1) all lie in wave 0's first pass; that wave
+//    takes the wrapped order (STRICT) or the masked index (FMA), the others plain u - t.
+// Same sums in the same order as cascade_fwd / cascade_rev (bit-identical in STRICT).
+// ---------------------------------------------------------------------------------------
+constexpr int kRowN = 4096;
+
+template <bool FMA, int M, int H>
+__device__ __forceinline__ void row_fwd_level(double* buf, double* ys, int tid, const Filters& f) {
+  constexpr int half = H / 2, P = half >= kNT2 ? half / kNT2 : 1, PAD = M - 2;
+  constexpr bool padded = H >= PAD;  // single wrap, read from the copy after the end
+  double lo[P], hi[P];
+#pragma unroll
+  for (int r = 0; r < P; ++r) {
+    const int i = tid + r * kNT2;
+    lo[r] = 0.;
+    hi[r] = 0.;
+    if (half >= kNT2 || i < half) {
+#pragma unroll
+      for (int t = 0; t < (M >> 1); ++t) {
+        const int k = padded ? 2 * i + 2 * t : (2 * i + 2 * t) & (H - 1);
+        const d2 v = *(const d2*)&buf[k];
+        lo[r] = madd<FMA>(lo[r], f.sD[2 * t], v.x);
+        hi[r] = madd<FMA>(hi[r], f.wD[2 * t], v.x);
+        lo[r] = madd<FMA>(lo[r], f.sD[2 * t + 1], v.y);
+        hi[r] = madd<FMA>(hi[r], f.wD[2 * t + 1], v.y);
+      }
+    }
+  }
+  __syncthreads();  // every read of buf[0 .. H + PAD) is done
+#pragma unroll
+  for (int r = 0; r < P; ++r) {
+    const int i = tid + r * kNT2;
+    if (half >= kNT2 || i < half) {
+      buf[i] = lo[r];
+      ys[half + i] = hi[r];
+    }
+  }
+  // the next level's wrap copy (its first PAD inputs are this level's lo[0 .. PAD))
+  if constexpr (PAD > 0 && half >= PAD) {
+    if (tid < PAD) buf[half + tid] = lo[0];
+  }
+  __syncthreads();
+}
+
+// Levels H, H/2, ... while level and tw allow; returns the length of the part left in buf.
+template <bool FMA, int M, int H>
+__device__ __forceinline__ int row_fwd_from(double* buf, double* ys, int tid, int level, int tw,
+                                            const Filters& f) {
+  if constexpr (H < 2) {
+    return H;
+  } else {
+    if (level <= 0 || H < tw) return H;
+    row_fwd_level<FMA, M, H>(buf, ys, tid, f);
+    return row_fwd_from<FMA, M, H / 2>(buf, ys, tid, level - 1, tw, f);
+  }
+}
+
+template <bool FMA, int M>
+__global__ __launch_bounds__(kNT2) void fwt_fwd_row(const double* x, double* y, int level, int tw,
+                                                   Filters f) {
+  constexpr int PAD = M - 2;
+  __shared__ __attribute__((aligned(16))) double buf[kRowN + PAD + 2];
+  const int tid = threadIdx.x;
+  const double* xs = x + (long)blockIdx.x * kRowN;
+  double* ys = y + (long)blockIdx.x * kRowN;
+#pragma unroll
+  for (int r = 0; r < kRowN / (2 * kNT2); ++r) {
+    const int i = 2 * (tid + r * kNT2);
+    *(d2*)&buf[i] = *(const d2*)&xs[i];
+  }
+  if (PAD > 0 && tid < PAD) buf[kRowN + tid] = xs[tid];
+  __syncthreads();
+  const int hcur = row_fwd_from<FMA, M, kRowN>(buf, ys, tid, level, tw, f);
+  for (int i = tid; i < hcur; i += kNT2) ys[i] = buf[i];
+}
+
+template <bool FMA, int M, int KIND, int H>
+__device__ __forceinline__ void row_rev_level(double* buf, double* xs, int tid, const Filters& f,
+                                              const d2* tp) {
+  constexpr int half = H / 2, P = half >= kNT2 ? half / kNT2 : 1;
+  d2 o[P];
+  if constexpr (H < M) {  // multi-wrap: Java's loop replayed per output
+    if (tid < half) o[0] = rev_pair_wrapped<FMA, M, KIND>(buf, H, tid, f);
+  } else {
+#pragma unroll
+    for (int r = 0; r < P; ++r) {
+      const int u = tid + r * kNT2;
+      if (half >= kNT2 || u < half) {
+        if (r == 0 && tid < 64) {  // wave-uniform: the wave holding u < M/2 - 1 (<= 19)
+          if constexpr (FMA) {
+            double a0 = 0., a1 = 0.;
+#pragma unroll
+            for (int t = (M >> 1) - 1; t >= 0; --t) {
+              const int i = (u - t) & (half - 1);
+              const double av = buf[i], dv = buf[i + half];
+              a0 = rev_acc<FMA, KIND>(a0, av, dv, f.sR[2 * t], f.wR[2 * t]);
+              a1 = rev_acc<FMA, KIND>(a1, av, dv, f.sR[2 * t + 1], f.wR[2 * t + 1]);
+            }
+            o[r] = d2{a0, a1};
+          } else {
+            o[r] = rev_pair_rot<FMA, M, KIND>(buf, H, u, tp);
+          }
+        } else {
+          double a0 = 0., a1 = 0.;
+#pragma unroll
+          for (int t = (M >> 1) - 1; t >= 0; --t) {
+            const double av = buf[u - t], dv = buf[u - t + half];
+            a0 = rev_acc<FMA, KIND>(a0, av, dv, f.sR[2 * t], f.wR[2 * t]);
+            a1 = rev_acc<FMA, KIND>(a1, av, dv, f.sR[2 * t + 1], f.wR[2 * t + 1]);
+          }
+          o[r] = d2{a0, a1};
+        }
+      }
+    }
+  }
+  if constexpr (H == kRowN) {  // last level: straight to global memory
+#pragma unroll
+    for (int r = 0; r < P; ++r) *(d2*)&xs[2 * (tid + r * kNT2)] = o[r];
+    return;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < P; ++r) {
+    const int u = tid + r * kNT2;
+    if (half >= kNT2 || u < half) *(d2*)&buf[2 * u] = o[r];
+  }
+  __syncthreads();
+}
+
+// Levels H, 2H, ..., kRowN from h0 on (h0 a power of two); true when the last one stored to xs.
+template <bool FMA, int M, int KIND, int H>
+__device__ __forceinline__ bool row_rev_from(double* buf, double* xs, int tid, int h0,
+                                             const Filters& f, const d2* tp) {
+  if constexpr (H > kRowN) {
+    return false;
+  } else {
+    if (H >= h0) {
+      row_rev_level<FMA, M, KIND, H>(buf, xs, tid, f, tp);
+      if constexpr (H == kRowN) return true;
+    }
+    return row_rev_from<FMA, M, KIND, 2 * H>(buf, xs, tid, h0, f, tp);
+  }
+}
+
+template <bool FMA, int M, int KIND>
+__global__ __launch_bounds__(kNT2) void fwt_rev_row(const double* y, double* x, int h0, int tw,
+                                                   Filters f) {
+  __shared__ __attribute__((aligned(16))) double buf[kRowN];
+  __shared__ d2 tp[M];
+  const int tid = threadIdx.x;
+  const double* ys = y + (long)blockIdx.x * kRowN;
+  double* xs = x + (long)blockIdx.x * kRowN;
+#pragma unroll
+  for (int r = 0; r < kRowN / (2 * kNT2); ++r) {
+    const int i = 2 * (tid + r * kNT2);
+    *(d2*)&buf[i] = *(const d2*)&ys[i];
+  }
+  fill_rev_taps<M>(tp, tid, f);
+  __syncthreads();
+  // cascade_rev's loop: h = h0, 2 h0, ... while h <= n, h >= tw, h >= 2 (h0 >= tw here)
+  const bool stored = h0 >= tw && h0 >= 2 && h0 <= kRowN &&
+                      row_rev_from<FMA, M, KIND, 2>(buf, xs, tid, h0, f, tp);
+  if (!stored)
+    for (int i = 2 * tid; i < kRowN; i += 2 * kNT2) *(d2*)&xs[i] = *(const d2*)&buf[i];
+}
+
+// ---------------------------------------------------------------------------------------
 // Wavelet packet transform (WaveletPacketTransform.java:60-191): every level applies
 // Wavelet.forward / reverse to each of the n/h packets of length h, not just the first.
 // Same per-packet arithmetic as the FWT cascades above (bit-identical in STRICT).
@@ -766,13 +941,24 @@ __global__ __launch_bounds__(kNT) void transpose_kernel(const double* __restrict
 #define JW_FWT_LENGTHS(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20) X(22) X(24) \
   X(26) X(28) X(30) X(32) X(34) X(36) X(38) X(40)
 
+// 4096-sample rows use fwt_fwd_row / fwt_rev_row; env JW_FWT_ROW=0 keeps the runtime-level
+// cascades (A/B runs, tests).
+bool row_kernels() {
+  const char* e = std::getenv("JW_FWT_ROW");
+  return !(e && e[0] == '0');
+}
+
 template <bool FMA>
 bool launch_fwd2(int M, dim3 g, hipStream_t s, const double* x, double* y, int n, int level,
                  int tw, const Filters& f) {
+  const bool row = n == kRowN && row_kernels();
   switch (M) {
 #define JW_C(MM)                                                                          \
   case MM:                                                                                \
-    hipLaunchKernelGGL((fwt_fwd_lds2<FMA, MM>), g, dim3(kNT2), 0, s, x, y, n, level, tw, f); \
+    if (row)                                                                              \
+      hipLaunchKernelGGL((fwt_fwd_row<FMA, MM>), g, dim3(kNT2), 0, s, x, y, level, tw, f); \
+    else                                                                                  \
+      hipLaunchKernelGGL((fwt_fwd_lds2<FMA, MM>), g, dim3(kNT2), 0, s, x, y, n, level, tw, f); \
     return true;
     JW_FWT_LENGTHS(JW_C)
 #undef JW_C
@@ -784,10 +970,18 @@ bool launch_fwd2(int M, dim3 g, hipStream_t s, const double* x, double* y, int n
 template <bool FMA>
 bool launch_rev2(int M, dim3 g, hipStream_t s, const double* y, double* x, int n, int h0, int tw,
                  int kind, const Filters& f) {
+  // the compile-time-level row kernel runs levels h0, 2 h0, ..., n: h0 a power of two
+  const bool row = n == kRowN && (h0 & (h0 - 1)) == 0 && row_kernels();
   switch (M) {
 #define JW_C(MM)                                                                           \
   case MM:                                                                                 \
-    if (kind == JW_WAVELET_HAAR_ORTH)                                                      \
+    if (row && kind == JW_WAVELET_HAAR_ORTH)                                               \
+      hipLaunchKernelGGL((fwt_rev_row<FMA, MM, JW_WAVELET_HAAR_ORTH>), g, dim3(kNT2), 0, s, y, \
+                         x, h0, tw, f);                                                    \
+    else if (row)                                                                          \
+      hipLaunchKernelGGL((fwt_rev_row<FMA, MM, JW_WAVELET_GENERIC>), g, dim3(kNT2), 0, s, y, \
+                         x, h0, tw, f);                                                    \
+    else if (kind == JW_WAVELET_HAAR_ORTH)                                                 \
       hipLaunchKernelGGL((fwt_rev_lds2<FMA, MM, JW_WAVELET_HAAR_ORTH>), g, dim3(kNT2), 0, s, y, \
                          x, n, h0, tw, kind, f);                                           \
     else                                                                                   \

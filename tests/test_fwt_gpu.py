@@ -215,3 +215,26 @@ def test_fast_and_generic_lds_kernels_agree(wname, monkeypatch):
         rref = orc.fwt_reverse(ref, lvl, wv)
         assert bits_equal(y_fast, ref) and bits_equal(y_gen, ref), (n, lvl)
         assert bits_equal(r_fast, rref) and bits_equal(r_gen, rref), (n, lvl)
+
+
+@pytest.mark.parametrize("wname", CREATE2ARR + ["Haar1Orthogonal", "Legendre1", "Legendre3"])
+def test_row4096_kernels_bit_exact(wname, monkeypatch):
+    # n = 4096 rows run fwt_fwd_row / fwt_rev_row (compile-time level sizes, wrap copy, details
+    # straight to HBM); JW_FWT_ROW=0 runs the runtime-level cascades.  STRICT: both bit-identical
+    # to the oracle at every level count; FMA: the two kernels add the same fused products in
+    # the same order, so they agree bit for bit too.
+    wv = wavelet(wname)
+    f = FastWaveletTransform(wv)
+    fm = FastWaveletTransform(wv, arith="fma")
+    n = 4096
+    x = orc.fill_uniform(n, 29)
+    for lvl in [0, 1, 2, 5, 11, 12]:
+        ref = orc.fwt_forward(x, lvl, wv)
+        rref = orc.fwt_reverse(ref, lvl, wv)
+        assert bits_equal(f.forward(x, lvl), ref), lvl
+        assert bits_equal(f.reverse(ref, lvl), rref), lvl
+        yf, rf = fm.forward(x, lvl), fm.reverse(ref, lvl)
+        monkeypatch.setenv("JW_FWT_ROW", "0")
+        assert bits_equal(fm.forward(x, lvl), yf), lvl
+        assert bits_equal(fm.reverse(ref, lvl), rf), lvl
+        monkeypatch.delenv("JW_FWT_ROW")
