@@ -751,6 +751,7 @@ constexpr int kSW = 64;      // columns per strip workgroup (32 lanes x 2 column
 constexpr int kST = 32;      // output rows per strip workgroup
 constexpr int kTailNL = 16;  // columns per tail workgroup (128-byte row pieces)
 constexpr int kTailLen = 256;
+constexpr int kTailNT = 512; // threads per tail workgroup (32 per column): 1024 held one per CU
 
 struct Strip {  // one level's buffers, each [rows][cols] per matrix with its own matrix stride
   const double* src;  // forward: level input rows [0, h); reverse: approximations rows [0, h/2)
@@ -861,10 +862,10 @@ __global__ __launch_bounds__(256) void fwt_strip_rev(Strip s, Filters f) {
 // The remaining levels of kTailNL columns on rows [0, len) (len <= kTailLen), in LDS:
 // forward levels lvl_h0 = level count from h = len; reverse from h = lvl_h0 up to len.
 template <bool FMA, int M, bool REV, int KIND>
-__global__ __launch_bounds__(1024) void fwt_cols_tail(const double* in, double* out, int len,
+__global__ __launch_bounds__(kTailNT) void fwt_cols_tail(const double* in, double* out, int len,
                                                       int cols, long ms_in, long ms_out,
                                                       int lvl_h0, int tw, Filters f) {
-  constexpr int NTL = 1024 / kTailNL;
+  constexpr int NTL = kTailNT / kTailNL;
   constexpr int PAD = kTailLen + 2;  // 16-byte aligned lines; the transposed stores spread banks
   __shared__ __attribute__((aligned(16))) double bufs[kTailNL * PAD];
   __shared__ d2 tp[M];
@@ -875,7 +876,7 @@ __global__ __launch_bounds__(1024) void fwt_cols_tail(const double* in, double* 
   const int line0 = (int)(blockIdx.x % nchunk) * kTailNL;
   const double* src = in + mat * ms_in + line0;
   double* dst = out + mat * ms_out + line0;
-  for (int k = tid; k < len * kTailNL; k += 1024) {
+  for (int k = tid; k < len * kTailNL; k += kTailNT) {
     const int i = k / kTailNL, c = k % kTailNL;
     bufs[c * PAD + i] = src[(long)i * cols + c];
   }
@@ -886,7 +887,7 @@ __global__ __launch_bounds__(1024) void fwt_cols_tail(const double* in, double* 
   } else {
     cascade_fwd<FMA, M, NTL, kTailLen>(buf, len, lvl_h0, tw, lt, f);
   }
-  for (int k = tid; k < len * kTailNL; k += 1024) {
+  for (int k = tid; k < len * kTailNL; k += kTailNT) {
     const int i = k / kTailNL, c = k % kTailNL;
     dst[(long)i * cols + c] = bufs[c * PAD + i];
   }
@@ -1063,7 +1064,7 @@ template <bool FMA>
 bool launch_tail(int M, int kind, bool rev, hipStream_t s, const double* in, double* out, int len,
                  int cols, long ms_in, long ms_out, int lvl_h0, int tw, int batch,
                  const Filters& f) {
-  const dim3 g((unsigned)((long)batch * (cols / kTailNL))), b(1024);
+  const dim3 g((unsigned)((long)batch * (cols / kTailNL))), b(kTailNT);
   switch (M) {
 #define JW_C(MM)                                                                                \
   case MM:                                                                                      \
