@@ -15,6 +15,7 @@
 #include <cmath>
 #include <map>
 #include <mutex>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -565,16 +566,66 @@ struct InvIn2 {  // item = signal; Z: Q column-major spectra per signal
   }
 };
 
-// filter products F ((J+1) rows, scratch) -> pair tables P (2Q rows), spectra layout
-int pair_tables(const ModwtPlan& p, long N, int J, long N1, long N2, const Tables& T, cplx** P,
-                StreamAllocs& mem, hipStream_t s) {
+// filter products F ((J+1) rows, scratch) -> pair tables P (2Q rows), spectra layout.
+// P depends on the filters, N and J alone, so it is built once per (device, filters, N, J)
+// and kept, like the twiddle and chirp-z tables: the first call for a key synchronises its
+// stream once (other streams may read the table right after), later calls launch no table
+// kernels (the two took ~0.4 ms per call at N = 2^20, J = 8).  At most kPairCacheBytes of
+// tables are kept; past that a new key gets a per-call table.
+struct PairKey {
+  int dev, L, J;
+  long N, N1;
+  std::vector<double> taps;  // g then h, L each: the plan's content, not its address
+  bool operator<(const PairKey& o) const {
+    return std::tie(dev, L, J, N, N1, taps) < std::tie(o.dev, o.L, o.J, o.N, o.N1, o.taps);
+  }
+};
+constexpr size_t kPairCacheBytes = 4UL << 30;
+std::mutex g_pair_mu;
+std::map<PairKey, cplx*> g_pair;
+size_t g_pair_bytes = 0;
+
+int build_pair_tables(const ModwtPlan& p, long N, int J, long N1, long N2, const Tables& T,
+                      cplx* P, StreamAllocs& mem, hipStream_t s) {
   cplx* F = nullptr;
   int st = products(p, N, J, N1, N2, T, &F, mem, s);
   if (st != JW_OK) return st;
-  const int Q = (J + 2) / 2;
-  JW_HIP_TRY(mem.alloc(P, (size_t)2 * Q * N * sizeof(cplx)));
-  hipLaunchKernelGGL(pair_products, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, *P, F, N, J);
+  hipLaunchKernelGGL(pair_products, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, P, F, N, J);
   JW_HIP_TRY(hipGetLastError());
+  return JW_OK;
+}
+
+int pair_tables(const ModwtPlan& p, long N, int J, long N1, long N2, const Tables& T, cplx** P,
+                StreamAllocs& mem, hipStream_t s) {
+  const int Q = (J + 2) / 2;
+  const size_t bytes = (size_t)2 * Q * N * sizeof(cplx);
+  PairKey key{0, p.L, J, N, N1, {}};
+  JW_HIP_TRY(hipGetDevice(&key.dev));
+  key.taps.assign(p.g, p.g + p.L);
+  key.taps.insert(key.taps.end(), p.h, p.h + p.L);
+  std::lock_guard<std::mutex> lk(g_pair_mu);
+  auto it = g_pair.find(key);
+  if (it != g_pair.end()) {
+    *P = it->second;
+    return JW_OK;
+  }
+  if (g_pair_bytes + bytes > kPairCacheBytes) {  // cache full: a table for this call only
+    JW_HIP_TRY(mem.alloc(P, bytes));
+    return build_pair_tables(p, N, J, N1, N2, T, *P, mem, s);
+  }
+  cplx* tab = nullptr;
+  JW_HIP_TRY(hipMalloc((void**)&tab, bytes));
+  int st = build_pair_tables(p, N, J, N1, N2, T, tab, mem, s);
+  hipError_t e = st == JW_OK ? hipStreamSynchronize(s) : hipSuccess;
+  if (st != JW_OK || e != hipSuccess) {
+    (void)hipFree(tab);
+    return st != JW_OK ? st
+                       : fail(JW_ERR_DEVICE, "MODWT FFT pair tables for N=%ld: %s", N,
+                              hipGetErrorString(e));
+  }
+  g_pair.emplace(std::move(key), tab);
+  g_pair_bytes += bytes;
+  *P = tab;
   return JW_OK;
 }
 
