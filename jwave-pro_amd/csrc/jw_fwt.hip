@@ -542,7 +542,15 @@ __global__ __launch_bounds__(kNT2) void fwt_rev_row(const double* y, double* x, 
     const int i = 2 * (tid + r * kNT2);
     *(d2*)&buf[i] = *(const d2*)&ys[i];
   }
-  fill_rev_taps<M>(tp, tid, f);
+  // fill_rev_taps with compile-time tap indices: a thread-indexed read of the kernel-argument
+  // filters made the compiler copy all 2 KB of them to scratch and read every tap from there
+#pragma unroll
+  for (int t = 0; t < M / 2; ++t) {
+    if (tid == t) {
+      tp[2 * t] = d2{f.sR[2 * t], f.sR[2 * t + 1]};
+      tp[2 * t + 1] = d2{f.wR[2 * t], f.wR[2 * t + 1]};
+    }
+  }
   __syncthreads();
   // cascade_rev's loop: h = h0, 2 h0, ... while h <= n, h >= tw, h >= 2 (h0 >= tw here)
   const bool stored = h0 >= tw && h0 >= 2 && h0 <= kRowN &&
@@ -939,8 +947,10 @@ __global__ __launch_bounds__(kNT) void transpose_kernel(const double* __restrict
 }
 
 // Even filter lengths with a compiled fast kernel; others use fwt_fwd_lds / fwt_rev_lds.
+#ifndef JW_FWT_LENGTHS  // (a one-length build for ISA inspection: -D'JW_FWT_LENGTHS(X)=X(16)')
 #define JW_FWT_LENGTHS(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20) X(22) X(24) \
   X(26) X(28) X(30) X(32) X(34) X(36) X(38) X(40)
+#endif
 
 // 4096-sample rows use fwt_fwd_row / fwt_rev_row; env JW_FWT_ROW=0 keeps the runtime-level
 // cascades (A/B runs, tests).
