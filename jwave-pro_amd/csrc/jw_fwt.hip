@@ -390,6 +390,7 @@ __global__ __launch_bounds__(kNT2) void fwt_rev_lds2(const double* __restrict__ 
 // Same sums in the same order as cascade_fwd / cascade_rev (bit-identical in STRICT).
 // ---------------------------------------------------------------------------------------
 constexpr int kRowN = 4096;
+constexpr int kRowMaxM = 20;  // longer filters keep the runtime-level kernels (compile time)
 
 template <bool FMA, int M, int H>
 __device__ __forceinline__ void row_fwd_level(double* buf, double* ys, int tid, const Filters& f) {
@@ -966,10 +967,13 @@ bool launch_fwd2(int M, dim3 g, hipStream_t s, const double* x, double* y, int n
   switch (M) {
 #define JW_C(MM)                                                                          \
   case MM:                                                                                \
-    if (row)                                                                              \
-      hipLaunchKernelGGL((fwt_fwd_row<FMA, MM>), g, dim3(kNT2), 0, s, x, y, level, tw, f); \
-    else                                                                                  \
-      hipLaunchKernelGGL((fwt_fwd_lds2<FMA, MM>), g, dim3(kNT2), 0, s, x, y, n, level, tw, f); \
+    if constexpr (MM <= kRowMaxM) {                                                       \
+      if (row) {                                                                          \
+        hipLaunchKernelGGL((fwt_fwd_row<FMA, MM>), g, dim3(kNT2), 0, s, x, y, level, tw, f); \
+        return true;                                                                      \
+      }                                                                                   \
+    }                                                                                     \
+    hipLaunchKernelGGL((fwt_fwd_lds2<FMA, MM>), g, dim3(kNT2), 0, s, x, y, n, level, tw, f); \
     return true;
     JW_FWT_LENGTHS(JW_C)
 #undef JW_C
@@ -986,13 +990,18 @@ bool launch_rev2(int M, dim3 g, hipStream_t s, const double* y, double* x, int n
   switch (M) {
 #define JW_C(MM)                                                                           \
   case MM:                                                                                 \
-    if (row && kind == JW_WAVELET_HAAR_ORTH)                                               \
-      hipLaunchKernelGGL((fwt_rev_row<FMA, MM, JW_WAVELET_HAAR_ORTH>), g, dim3(kNT2), 0, s, y, \
-                         x, h0, tw, f);                                                    \
-    else if (row)                                                                          \
-      hipLaunchKernelGGL((fwt_rev_row<FMA, MM, JW_WAVELET_GENERIC>), g, dim3(kNT2), 0, s, y, \
-                         x, h0, tw, f);                                                    \
-    else if (kind == JW_WAVELET_HAAR_ORTH)                                                 \
+    if constexpr (MM <= kRowMaxM) {                                                        \
+      if (row) {                                                                           \
+        if (kind == JW_WAVELET_HAAR_ORTH)                                                  \
+          hipLaunchKernelGGL((fwt_rev_row<FMA, MM, JW_WAVELET_HAAR_ORTH>), g, dim3(kNT2), 0, s, \
+                             y, x, h0, tw, f);                                             \
+        else                                                                               \
+          hipLaunchKernelGGL((fwt_rev_row<FMA, MM, JW_WAVELET_GENERIC>), g, dim3(kNT2), 0, s, \
+                             y, x, h0, tw, f);                                             \
+        return true;                                                                       \
+      }                                                                                    \
+    }                                                                                      \
+    if (kind == JW_WAVELET_HAAR_ORTH)                                                      \
       hipLaunchKernelGGL((fwt_rev_lds2<FMA, MM, JW_WAVELET_HAAR_ORTH>), g, dim3(kNT2), 0, s, y, \
                          x, n, h0, tw, kind, f);                                           \
     else                                                                                   \

@@ -220,7 +220,8 @@ def test_fast_and_generic_lds_kernels_agree(wname, monkeypatch):
 @pytest.mark.parametrize("wname", CREATE2ARR + ["Haar1Orthogonal", "Legendre1", "Legendre3"])
 def test_row4096_kernels_bit_exact(wname, monkeypatch):
     # n = 4096 rows run fwt_fwd_row / fwt_rev_row (compile-time level sizes, wrap copy, details
-    # straight to HBM); JW_FWT_ROW=0 runs the runtime-level cascades.  STRICT: both bit-identical
+    # straight to HBM) for filters of up to 20 taps; JW_FWT_ROW=0 runs the runtime-level
+    # cascades (which longer filters always use).  STRICT: both bit-identical
     # to the oracle at every level count; FMA: the two kernels add the same fused products in
     # the same order, so they agree bit for bit too.
     wv = wavelet(wname)
