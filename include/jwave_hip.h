@@ -92,6 +92,15 @@ int jw_fft_forward(const double* in_reim, double* out_reim, long n, int batch, i
                    void* stream);
 int jw_fft_reverse(const double* in_reim, double* out_reim, long n, int batch, int where,
                    void* stream);
+/* The same transforms under an arithmetic contract.  JW_ARITH_STRICT runs the reference's own
+ * algorithm operation for operation -- bit reversal, radix-2 decimation in time with the
+ * recurrence twiddles wn = wn.mul(w) of every stage (:172-212), Complex.mul's (ac - bd, ad + bc)
+ * -- so results are the JVM's bit for bit for power-of-two n <= 2^24.  JW_ARITH_FMA is
+ * jw_fft_forward / jw_fft_reverse (correctly rounded twiddle tables). */
+int jw_fft_forward_ex(const double* in_reim, double* out_reim, long n, int batch, int arith,
+                      int where, void* stream);
+int jw_fft_reverse_ex(const double* in_reim, double* out_reim, long n, int batch, int arith,
+                      int where, void* stream);
 
 /* ======================================================================
  * FWT  (replaces FastWaveletTransform.forward/reverse(double[], level) :71/:119,

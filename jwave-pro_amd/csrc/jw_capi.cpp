@@ -289,18 +289,30 @@ static bool auto_level_fft(long n, int L, int j, int threshold) {
   return prod > threshold;
 }
 
-// FFT runs the frequency-domain pyramid (jw_modwt_fft.hip).  AUTO runs it when the reference's
-// rule sends any level's convolution to its FFT path (the pyramid is evaluated as a whole in
-// the frequency domain, so a plan mixing DIRECT and FFT levels runs entirely as FFT: the DIRECT
-// levels' values agree to rounding) and the exact direct kernels otherwise.  Lengths outside
-// the FFT engine's range run DIRECT.
-static bool use_fft(const ModwtPlan& p, int method, long n, int levels) {
-  if (!modwt_fft_supported(n)) return false;
-  if (method == JW_CONV_FFT) return true;
-  if (method != JW_CONV_AUTO) return false;
-  for (int j = 1; j <= levels; ++j)
-    if (auto_level_fft(n, p.L, j, p.fft_threshold)) return true;
-  return false;
+// Which implementation runs a MODWT call.
+//   JW_ARITH_STRICT (the JVM's arithmetic): every level takes the convolution the reference's
+//     performConvolution takes (:640-664) -- FFT always, DIRECT never, AUTO by the int32
+//     N*M_j > fftConvolutionThreshold rule -- and FFT levels run the reference's own FFT
+//     (jw_jfft.hip), so results are the JVM's bit for bit.  Lengths that path does not take yet
+//     run the exact-twiddle pyramid (jw_modwt_fft.hip) when any level is FFT.
+//   JW_ARITH_FMA (fast contract): FFT runs the exact-twiddle frequency-domain pyramid; AUTO and
+//     DIRECT run the direct kernels, which are faster and more accurate than any FFT path here.
+enum class ModwtPath { kDirect, kStrictLevels, kPyramid };
+
+static ModwtPath modwt_path(const ModwtPlan& p, int method, long n, int levels, bool* fft) {
+  bool any = false;
+  for (int j = 1; j <= levels; ++j) {
+    fft[j] = method == JW_CONV_FFT ||
+             (method == JW_CONV_AUTO && auto_level_fft(n, p.L, j, p.fft_threshold));
+    any = any || fft[j];
+  }
+  if (p.arith == JW_ARITH_FMA) {
+    return method == JW_CONV_FFT && modwt_fft_supported(n) ? ModwtPath::kPyramid
+                                                           : ModwtPath::kDirect;
+  }
+  if (!any) return ModwtPath::kDirect;
+  if (modwt_strict_fft_supported(n)) return ModwtPath::kStrictLevels;
+  return modwt_fft_supported(n) ? ModwtPath::kPyramid : ModwtPath::kDirect;
 }
 
 int jw_modwt_forward(const jw_modwt_plan* plan, const double* x, double* coeffs, long n,
@@ -333,9 +345,15 @@ int jw_modwt_forward(const jw_modwt_plan* plan, const double* x, double* coeffs,
   const size_t nin = (size_t)n * batch, nout = (size_t)n * batch * (levels + 1);
   return run(where, stream, x, nin, coeffs, nout,
              [&](const double* dx, double* dc, hipStream_t s) {
-               return use_fft(*plan, method, n, levels)
-                          ? modwt_forward_fft_device(*plan, dx, dc, n, levels, batch, s)
-                          : modwt_forward_device(*plan, dx, dc, n, levels, batch, s);
+               bool fft[kMaxModwtLevel + 1] = {};
+               switch (modwt_path(*plan, method, n, levels, fft)) {
+                 case ModwtPath::kStrictLevels:
+                   return modwt_forward_strict_device(*plan, dx, dc, n, levels, batch, fft, s);
+                 case ModwtPath::kPyramid:
+                   return modwt_forward_fft_device(*plan, dx, dc, n, levels, batch, s);
+                 default:
+                   return modwt_forward_device(*plan, dx, dc, n, levels, batch, s);
+               }
              });
 }
 
@@ -359,18 +377,26 @@ int jw_modwt_inverse(const jw_modwt_plan* plan, const double* coeffs, double* x,
   const size_t nin = (size_t)n * batch * (levels + 1), nout = (size_t)n * batch;
   return run(where, stream, coeffs, nin, x, nout,
              [&](const double* dc, double* dx, hipStream_t s) {
-               return use_fft(*plan, method, n, levels)
-                          ? modwt_inverse_fft_device(*plan, dc, dx, n, levels, batch, s)
-                          : modwt_inverse_device(*plan, dc, dx, n, levels, batch, s);
+               bool fft[kMaxModwtLevel + 1] = {};
+               switch (modwt_path(*plan, method, n, levels, fft)) {
+                 case ModwtPath::kStrictLevels:
+                   return modwt_inverse_strict_device(*plan, dc, dx, n, levels, batch, fft, s);
+                 case ModwtPath::kPyramid:
+                   return modwt_inverse_fft_device(*plan, dc, dx, n, levels, batch, s);
+                 default:
+                   return modwt_inverse_device(*plan, dc, dx, n, levels, batch, s);
+               }
              });
 }
 
 // ---------------------------------------------------------------- FFT
 // FastFourierTransform.forward / reverse(Complex[]) (FastFourierTransform.java:112-164):
 // length 0 -> nothing, 1 -> a copy, powers of two -> Cooley-Tukey, others -> Bluestein.
-static int fft_call(int S, const double* in, double* out, long n, int batch, int where,
+static int fft_call(int S, int arith, const double* in, double* out, long n, int batch, int where,
                     void* stream) {
   clear_error();
+  if (arith != JW_ARITH_STRICT && arith != JW_ARITH_FMA)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "unknown arithmetic mode %d", arith);
   if (n < 0 || batch < 0)
     return fail(JW_ERR_ILLEGAL_ARGUMENT, "negative length %ld or batch %d", n, batch);
   int st = check_where(where);
@@ -378,19 +404,32 @@ static int fft_call(int S, const double* in, double* out, long n, int batch, int
   if (n == 0 || batch == 0) return JW_OK;
   if (!in || !out) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
   const size_t elems = (size_t)2 * n * batch;
+  // STRICT: the reference's own FFT (jw_jfft.hip) for power-of-two n <= 2^24
+  const bool strict = arith == JW_ARITH_STRICT && (n & (n - 1)) == 0 && n <= (1L << 24);
   return run(where, stream, in, elems, out, elems, [&](const double* di, double* dout, hipStream_t s) {
-    return fft_device(S, di, dout, n, batch, s);
+    return strict ? fft_strict_device(S, di, dout, n, batch, s)
+                  : fft_device(S, di, dout, n, batch, s);
   });
 }
 
 int jw_fft_forward(const double* in_reim, double* out_reim, long n, int batch, int where,
                    void* stream) {
-  return fft_call(-1, in_reim, out_reim, n, batch, where, stream);
+  return fft_call(-1, JW_ARITH_FMA, in_reim, out_reim, n, batch, where, stream);
 }
 
 int jw_fft_reverse(const double* in_reim, double* out_reim, long n, int batch, int where,
                    void* stream) {
-  return fft_call(1, in_reim, out_reim, n, batch, where, stream);
+  return fft_call(1, JW_ARITH_FMA, in_reim, out_reim, n, batch, where, stream);
+}
+
+int jw_fft_forward_ex(const double* in_reim, double* out_reim, long n, int batch, int arith,
+                      int where, void* stream) {
+  return fft_call(-1, arith, in_reim, out_reim, n, batch, where, stream);
+}
+
+int jw_fft_reverse_ex(const double* in_reim, double* out_reim, long n, int batch, int arith,
+                      int where, void* stream) {
+  return fft_call(1, arith, in_reim, out_reim, n, batch, where, stream);
 }
 
 // ---------------------------------------------------------------- FWT

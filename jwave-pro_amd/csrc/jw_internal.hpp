@@ -103,6 +103,25 @@ int modwt_forward_fft_device(const ModwtPlan& p, const double* x, double* coeffs
                              int batch, hipStream_t s);
 int modwt_inverse_fft_device(const ModwtPlan& p, const double* coeffs, double* x, long n, int J,
                              int batch, hipStream_t s);
+// JW_ARITH_STRICT FFT paths (jw_jfft.hip): the reference's own FFT, bit for bit.
+// MODWT with fft_level[j] (j = 1..J) choosing each level's convolution like
+// performConvolution (MODWTTransform.java:640-664); DIRECT levels run modwt_level_*_device.
+bool modwt_strict_fft_supported(long n);
+int modwt_forward_strict_device(const ModwtPlan& p, const double* x, double* coeffs, long n,
+                                int J, int batch, const bool* fft_level, hipStream_t s);
+int modwt_inverse_strict_device(const ModwtPlan& p, const double* coeffs, double* x, long n,
+                                int J, int batch, const bool* fft_level, hipStream_t s);
+int fft_strict_device(int S, const double* in, double* out, long n, long batch, hipStream_t s);
+// Frees the cached twiddle / filter-spectrum / chirp tables of every FFT path (bytes freed).
+size_t release_strict_caches();
+size_t release_fft_caches();
+// One direct MODWT level (circularConvolve{,Adjoint}, :677-716) on batch rows with strides:
+// forward W_j, V_j <- V_{j-1}; inverse out = g_j^T V_j + h_j^T W_j.
+int modwt_level_forward_device(const ModwtPlan& p, int j, const double* v, long vs, double* w,
+                               long ws, double* vn, long vns, long N, int batch, hipStream_t s);
+int modwt_level_inverse_device(const ModwtPlan& p, int j, const double* v, long vs,
+                               const double* w, long ws, double* out, long os, long N, int batch,
+                               hipStream_t s);
 // FastFourierTransform.forward (S = -1) / reverse (S = +1, scaled by 1/n) of batch lines of n
 // interleaved complex values in HBM; in == out allowed.
 int fft_device(int S, const double* in, double* out, long n, long batch, hipStream_t s);

@@ -1,0 +1,442 @@
+// jw_jfft.hpp -- the reference's own FFT, operation for operation, on gfx950 (JW_ARITH_STRICT).
+//
+// FastFourierTransform.fftCooleyTukey (src/main/java/jwave/transforms/FastFourierTransform.java
+// :172-212) is a radix-2 decimation-in-time FFT: bit reversal (Integer.reverse, :176-184), then
+// for size = 2, 4, .., n every block's butterflies
+//     t = wn.mul(x[k + half]);  x[k] = u.add(t);  x[k + half] = u.sub(t);  wn = wn.mul(w)
+// with w = (Math.cos(a), Math.sin(a)), a = 2 pi / size * (inverse ? 1 : -1), and wn restarting at
+// (1, 0) in every block (:188-202).  Every block of one stage therefore uses the same twiddle
+// sequence wn_k, k < half, built by the recurrence: the host tabulates it once per n in that
+// order (Tw[half + k] = wn_k), so each butterfly here is the JVM's exact IEEE sequence
+// (Complex.mul = (ac - bd, ad + bc), Complex.java:286-288; no FMA: -ffp-contract=off).  Grouping
+// the butterflies of several stages in registers changes no operation, so the result is the
+// reference's bit for bit.
+//
+// Geometry.  A transform of n = R x C (R, C powers of two) runs as two "column" passes:
+//   pass 1: column c of the natural-order input viewed as [R][C] (x[r C + c]) is the block of
+//           positions rev(c) R .. rev(c) R + R - 1 after the global bit reversal, placed at
+//           rev_R(r): stages 1..log R on it, stored as row rev_C(c) of Z ([C][R], contiguous);
+//   pass 2: column l of Z (Z[h R + l], h < C): stages log R + 1..log n pair h with h + 2^t and
+//           take the twiddle Tw[(2^t + h mod 2^t) R + l]; the result is X[h R + l] in natural
+//           order -- which is column l of the next transform's pass-1 view when that one splits
+//           n as C x R (so a pass 2 can feed the next transform's pass 1 without HBM).
+// The pass-2 twiddles are stored transposed (Tw2[l][m] = Tw[m R + l]) so that the lanes of one
+// column read consecutive entries.  Short transforms (n <= 4096) run whole in one "column".
+//
+// A column of LC points is held by LC/EPT threads with EPT = min(16, LC) points each; a
+// workgroup of 256 threads holds T = 256 EPT / LC columns in LDS (padded: one slot per 16
+// points, one per column).  Stages run in register groups of up to 4 (radix 16).
+#pragma once
+#include "jw_internal.hpp"
+
+namespace jw {
+namespace jf {
+
+using cplx = double2;
+constexpr int kNT = 256;
+
+__host__ __device__ constexpr int ilog2(long v) {
+  int r = 0;
+  while ((1L << r) < v) ++r;
+  return r;
+}
+
+template <int LC>
+struct Geo {
+  static constexpr int LOG = ilog2(LC);
+  static constexpr int EPT = LC < 16 ? LC : 16;
+  static constexpr int GMAX = ilog2(EPT);
+  static constexpr int TPC = LC / EPT;  // threads per column (divides 64 when <= 64)
+  static constexpr int T = kNT / TPC;   // columns per workgroup
+  static constexpr int CS = LC + LC / 16 + 1;
+  static constexpr size_t LDS_BYTES = (size_t)T * CS * sizeof(cplx);
+};
+
+__device__ __forceinline__ int pidx(int pos) { return pos + (pos >> 4); }
+__device__ __forceinline__ int brev(int v, int bits) {
+  return bits == 0 ? 0 : (int)(__builtin_bitreverse32((unsigned)v) >> (32 - bits));
+}
+
+// Complex.mul(Complex) :286-288 and mul(double) :299-301
+__device__ __forceinline__ cplx jmul(cplx a, cplx b) {
+  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ cplx jscale(cplx a, double s) { return make_double2(a.x * s, a.y * s); }
+// one butterfly of fftCooleyTukey :196-199 (t = wn.mul(x[k + half]))
+__device__ __forceinline__ void bfly(cplx& u, cplx& v, cplx w) {
+  const cplx t = jmul(w, v);
+  const cplx a = u;
+  u = make_double2(a.x + t.x, a.y + t.y);
+  v = make_double2(a.x - t.x, a.y - t.y);
+}
+
+template <int LC>
+__device__ __forceinline__ void col_sync() {
+  if constexpr (Geo<LC>::TPC <= 64) {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  } else {
+    __syncthreads();
+  }
+}
+
+// Stages t0 .. t0+G-1 of one column (positions j; stage t pairs j, j + 2^t with bit t clear and
+// uses tw[2^t + (j mod 2^t)]).  Thread tl owns EPT/2^G sets {base + m 2^t0 : m < 2^G}.
+template <int LC, int G>
+__device__ __forceinline__ void stage_group(cplx* __restrict__ col, int tl, int t0,
+                                            const cplx* __restrict__ tw) {
+  using Gm = Geo<LC>;
+  constexpr int E = 1 << G, NSET = Gm::EPT / E;
+  cplx v[Gm::EPT];
+  int base[NSET];
+  const int lowmask = (1 << t0) - 1;
+#pragma unroll
+  for (int i = 0; i < NSET; ++i) {
+    const int set = tl + Gm::TPC * i;
+    base[i] = (set & lowmask) + ((set >> t0) << (t0 + G));
+#pragma unroll
+    for (int m = 0; m < E; ++m) v[i * E + m] = col[pidx(base[i] + (m << t0))];
+  }
+#pragma unroll
+  for (int u = 0; u < G; ++u) {
+#pragma unroll
+    for (int i = 0; i < NSET; ++i) {
+      const int low = base[i] & lowmask;
+#pragma unroll
+      for (int r = 0; r < (1 << u); ++r) {
+        const cplx w = tw[(1 << (t0 + u)) + low + (r << t0)];
+#pragma unroll
+        for (int q = 0; q < (E >> (u + 1)); ++q) {
+          const int m = r + (q << (u + 1));
+          bfly(v[i * E + m], v[i * E + m + (1 << u)], w);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NSET; ++i) {
+#pragma unroll
+    for (int m = 0; m < E; ++m) col[pidx(base[i] + (m << t0))] = v[i * E + m];
+  }
+}
+
+// all LOG stages of one column, in groups of GMAX (the column's points must be in place)
+template <int LC, int T0 = 0>
+__device__ __forceinline__ void run_stages(cplx* __restrict__ col, int tl,
+                                           const cplx* __restrict__ tw) {
+  using Gm = Geo<LC>;
+  if constexpr (T0 < Gm::LOG) {
+    constexpr int G = (Gm::LOG - T0) < Gm::GMAX ? (Gm::LOG - T0) : Gm::GMAX;
+    if constexpr (T0 > 0) col_sync<LC>();
+    stage_group<LC, G>(col, tl, T0, tw);
+    run_stages<LC, T0 + G>(col, tl, tw);
+  }
+}
+
+// the thread's own points of its column: positions tl + TPC k
+template <int LC>
+__device__ __forceinline__ int own_pos(int tl, int k) {
+  return tl + Geo<LC>::TPC * k;
+}
+
+// Workgroup -> (column tile, item).  When the tiles split evenly over the 8 XCDs, every XCD
+// takes its own tiles and runs all items of a tile back to back, so the tile's pass-2
+// twiddles and filter-spectrum columns stay in that XCD's L2.
+__device__ __forceinline__ void tile_item(int ntiles, long nitems, int* tile, long* item) {
+  const long b = (long)blockIdx.x + (long)blockIdx.y * gridDim.x;
+  if ((ntiles & 7) == 0) {
+    const int xcd = (int)(b & 7);
+    const long q = b >> 3;
+    *item = q % nitems;
+    *tile = xcd * (ntiles >> 3) + (int)(q / nitems);
+  } else {
+    *tile = (int)(b % ntiles);
+    *item = b / ntiles;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Column passes.  Every functor addresses an item's points by natural index: In is
+// cplx operator()(long item, long i) with i = r W + c for point (r, c) of the [LC][W] view
+// (W = 2^wbits columns); outputs are operator()(long item, long i, cplx v), where a row store
+// (Z, the pass-1 result) writes i = row LC + pos, row = rev(column).
+// ---------------------------------------------------------------------------------------
+template <int LC, bool REV, class In>
+__device__ __forceinline__ void load_cols(cplx* lds, const In& in, long item, int c0, int wbits) {
+  using G = Geo<LC>;
+  cplx v[G::EPT];
+#pragma unroll
+  for (int k = 0; k < G::EPT; ++k) {
+    const int f = threadIdx.x + kNT * k;
+    v[k] = in(item, ((long)(f / G::T) << wbits) + c0 + f % G::T);
+  }
+#pragma unroll
+  for (int k = 0; k < G::EPT; ++k) {
+    const int f = threadIdx.x + kNT * k;
+    const int r = f / G::T;
+    lds[(f % G::T) * G::CS + pidx(REV ? brev(r, G::LOG) : r)] = v[k];
+  }
+}
+
+template <int LC, class Out>
+__device__ __forceinline__ void store_rows(const cplx* lds, const Out& out, long item, int c0,
+                                           int wbits) {
+  using G = Geo<LC>;
+#pragma unroll
+  for (int k = 0; k < G::EPT; ++k) {
+    const int f = threadIdx.x + kNT * k;
+    const int cc = f / LC, pos = f % LC;
+    out(item, (long)brev(c0 + cc, wbits) * LC + pos, lds[cc * G::CS + pidx(pos)]);
+  }
+}
+
+template <int LC, class Out>
+__device__ __forceinline__ void store_cols(const cplx* lds, const Out& out, long item, int c0,
+                                           int wbits) {
+  using G = Geo<LC>;
+#pragma unroll
+  for (int k = 0; k < G::EPT; ++k) {
+    const int f = threadIdx.x + kNT * k;
+    const int cc = f % G::T, r = f / G::T;
+    out(item, ((long)r << wbits) + c0 + cc, lds[cc * G::CS + pidx(r)]);
+  }
+}
+
+// pass 1: columns of [LC][W] (bit-reversed into LDS), stages with the natural table, rows of Z
+template <int LC, class In, class Out>
+__global__ __launch_bounds__(kNT) void kp1(In in, Out out, int wbits, long nitems,
+                                           const cplx* __restrict__ tw1) {
+  using G = Geo<LC>;
+  extern __shared__ cplx lds[];
+  int tile;
+  long item;
+  tile_item((1 << wbits) / G::T, nitems, &tile, &item);
+  const int c0 = tile * G::T;
+  load_cols<LC, true>(lds, in, item, c0, wbits);
+  __syncthreads();
+  const int cc = threadIdx.x / G::TPC, tl = threadIdx.x % G::TPC;
+  run_stages<LC>(lds + cc * G::CS, tl, tw1);
+  __syncthreads();
+  store_rows<LC>(lds, out, item, c0, wbits);
+}
+
+// pass 2, natural-order output through Out (the spectrum, or a real row)
+template <int LC, class In, class Out>
+__global__ __launch_bounds__(kNT) void kp2s(In in, Out out, int wbits, long nitems,
+                                            const cplx* __restrict__ tw2) {
+  using G = Geo<LC>;
+  extern __shared__ cplx lds[];
+  int tile;
+  long item;
+  tile_item((1 << wbits) / G::T, nitems, &tile, &item);
+  const int c0 = tile * G::T;
+  load_cols<LC, false>(lds, in, item, c0, wbits);
+  __syncthreads();
+  const int cc = threadIdx.x / G::TPC, tl = threadIdx.x % G::TPC;
+  run_stages<LC>(lds + cc * G::CS, tl, tw2 + (long)(c0 + cc) * LC);
+  __syncthreads();
+  store_cols<LC>(lds, out, item, c0, wbits);
+}
+
+// pass 2, then NF pointwise products (Mid: cplx operator()(int f, long item, long i, cplx X),
+// i = the natural index h W + l), each run through pass 1 of the next transform (table tw1)
+// and stored as rows (Out: operator()(int f, long item, long j, cplx v), j = row LC + pos).
+template <int LC, int NF, class In, class Mid, class Out>
+__global__ __launch_bounds__(kNT) void kp2p(In in, Mid mid, Out out, int wbits, long nitems,
+                                            const cplx* __restrict__ tw2,
+                                            const cplx* __restrict__ tw1) {
+  using G = Geo<LC>;
+  extern __shared__ cplx lds[];
+  int tile;
+  long item;
+  tile_item((1 << wbits) / G::T, nitems, &tile, &item);
+  const int c0 = tile * G::T;
+  load_cols<LC, false>(lds, in, item, c0, wbits);
+  __syncthreads();
+  const int cc = threadIdx.x / G::TPC, tl = threadIdx.x % G::TPC;
+  cplx* col = lds + cc * G::CS;
+  run_stages<LC>(col, tl, tw2 + (long)(c0 + cc) * LC);
+  col_sync<LC>();
+  cplx X[G::EPT];
+#pragma unroll
+  for (int k = 0; k < G::EPT; ++k) X[k] = col[pidx(own_pos<LC>(tl, k))];
+  const long l = c0 + cc;
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    if (f == 0) {
+      col_sync<LC>();
+    } else {
+      __syncthreads();
+    }
+#pragma unroll
+    for (int k = 0; k < G::EPT; ++k) {
+      const int h = own_pos<LC>(tl, k);
+      col[pidx(brev(h, G::LOG))] = mid(f, item, ((long)h << wbits) + l, X[k]);
+    }
+    col_sync<LC>();
+    run_stages<LC>(col, tl, tw1);
+    __syncthreads();
+    store_rows<LC>(lds, [&](long it, long j, cplx v) { out(f, it, j, v); }, item, c0, wbits);
+  }
+}
+
+// pass 2 of NIN inverse transforms of one item (In: cplx operator()(int s, long item, long i)),
+// each reduced to a real value by Post (double operator()(int s, long item, long i, cplx v)),
+// summed in stream order (the
+// reference's vFromApprox[i] + vFromDetail[i], MODWTTransform.java:366-369).  FUSE: the sum
+// (as Complex(v, 0)) runs through pass 1 of the next forward transform (table tw1f) and is
+// stored as rows (Out: operator()(long item, long j, cplx v)); otherwise Out
+// (operator()(long item, long i, double v)) stores it at natural index i.
+template <int LC, int NIN, bool FUSE, class In, class Post, class Out>
+__global__ __launch_bounds__(kNT) void kp2r(In in, Post post, Out out, int wbits, long nitems,
+                                            const cplx* __restrict__ tw2,
+                                            const cplx* __restrict__ tw1f) {
+  using G = Geo<LC>;
+  extern __shared__ cplx lds[];
+  int tile;
+  long item;
+  tile_item((1 << wbits) / G::T, nitems, &tile, &item);
+  const int c0 = tile * G::T;
+  const int cc = threadIdx.x / G::TPC, tl = threadIdx.x % G::TPC;
+  cplx* col = lds + cc * G::CS;
+  const long l = c0 + cc;
+  double acc[G::EPT];
+#pragma unroll
+  for (int s = 0; s < NIN; ++s) {
+    if (s > 0) __syncthreads();
+    load_cols<LC, false>(lds, [&](long it, long i) { return in(s, it, i); }, item, c0, wbits);
+    __syncthreads();
+    run_stages<LC>(col, tl, tw2 + l * LC);
+    col_sync<LC>();
+#pragma unroll
+    for (int k = 0; k < G::EPT; ++k) {
+      const int h = own_pos<LC>(tl, k);
+      const double v = post(s, item, ((long)h << wbits) + l, col[pidx(h)]);
+      acc[k] = s == 0 ? v : acc[k] + v;
+    }
+  }
+  col_sync<LC>();
+  if constexpr (FUSE) {
+#pragma unroll
+    for (int k = 0; k < G::EPT; ++k)
+      col[pidx(brev(own_pos<LC>(tl, k), G::LOG))] = make_double2(acc[k], 0.0);
+    col_sync<LC>();
+    run_stages<LC>(col, tl, tw1f);
+    __syncthreads();
+    store_rows<LC>(lds, out, item, c0, wbits);
+  } else {
+#pragma unroll
+    for (int k = 0; k < G::EPT; ++k) col[pidx(own_pos<LC>(tl, k))] = make_double2(acc[k], 0.0);
+    __syncthreads();
+    store_cols<LC>(lds, [&](long it, long i, cplx v) { out(it, i, v.x); }, item, c0, wbits);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Whole transforms in one column (n = LC <= 4096): T lines per workgroup, the line's points
+// loaded by its own threads (positions tl + TPC k: coalesced), so only column syncs.
+// ---------------------------------------------------------------------------------------
+// load line `line` (In: cplx operator()(long line, int r)) bit-reversed into col
+template <int LC, class In>
+__device__ __forceinline__ void line_load_rev(cplx* col, int tl, const In& in, long line) {
+  using G = Geo<LC>;
+  cplx v[G::EPT];
+#pragma unroll
+  for (int k = 0; k < G::EPT; ++k) v[k] = in(line, own_pos<LC>(tl, k));
+#pragma unroll
+  for (int k = 0; k < G::EPT; ++k) col[pidx(brev(own_pos<LC>(tl, k), G::LOG))] = v[k];
+}
+
+// jw_fft (JW_ARITH_STRICT): In (line, r) -> cplx; Out (line, r, cplx); scale applied to both
+// parts when inverse (x[i].mul(1.0 / n), :207-211)
+template <int LC, class In, class Out>
+__global__ __launch_bounds__(kNT) void kline_fft(In in, Out out, long nlines,
+                                                 const cplx* __restrict__ tw, double scale,
+                                                 int do_scale) {
+  using G = Geo<LC>;
+  extern __shared__ cplx lds[];
+  const int cc = threadIdx.x / G::TPC, tl = threadIdx.x % G::TPC;
+  const long line = (long)blockIdx.x * G::T + cc;
+  const bool valid = line < nlines;  // no early exit: columns of 2048+ points sync the group
+  cplx* col = lds + cc * G::CS;
+  line_load_rev<LC>(col, tl, [&](long ln, int r) { return valid ? in(ln, r) : cplx{0.0, 0.0}; },
+                    line);
+  col_sync<LC>();
+  run_stages<LC>(col, tl, tw);
+  col_sync<LC>();
+  if (!valid) return;
+#pragma unroll
+  for (int k = 0; k < G::EPT; ++k) {
+    const int p = own_pos<LC>(tl, k);
+    cplx v = col[pidx(p)];
+    if (do_scale) v = jscale(v, scale);
+    out(line, p, v);
+  }
+}
+
+// One MODWT level on whole lines (n = LC <= 4096), MODWTTransform.java:290-304 / :355-372 with
+// circularConvolveFFT{,Adjoint} (:752-837): NIN input rows per line, each FFT'd (Complex(x, 0)),
+// multiplied by a filter spectrum (Mid: cplx operator()(int s, int f, long i, cplx X)), inverse
+// FFT'd and reduced to its real part times 1/n.
+//   forward (NIN = 1, NOUT = 2): row V_{j-1} -> W_j = Re IFFT(X Fh_j)/n, V_j = Re IFFT(X Fg_j)/n
+//   inverse (NIN = 2, NOUT = 1): V_{j-1} = Re IFFT(FFT(V_j) conj Fg_j)/n
+//                                        + Re IFFT(FFT(W_j) conj Fh_j)/n
+// In: double operator()(int s, long line, int r);  Out: operator()(int f, long line, int r, double)
+template <int LC, int NIN, int NOUT, class In, class Mid, class Out>
+__global__ __launch_bounds__(kNT) void kline_modwt(In in, Mid mid, Out out, long nlines,
+                                                   const cplx* __restrict__ twf,
+                                                   const cplx* __restrict__ twi, double inv_n) {
+  static_assert(NIN == 1 || NOUT == 1, "forward: 1 in / 2 out; inverse: 2 in / 1 out");
+  using G = Geo<LC>;
+  extern __shared__ cplx lds[];
+  const int cc = threadIdx.x / G::TPC, tl = threadIdx.x % G::TPC;
+  const long line = (long)blockIdx.x * G::T + cc;
+  const bool valid = line < nlines;
+  cplx* col = lds + cc * G::CS;
+  double acc[G::EPT];
+#pragma unroll
+  for (int s = 0; s < NIN; ++s) {
+    if (s > 0) col_sync<LC>();
+    line_load_rev<LC>(
+        col, tl,
+        [&](long ln, int r) { return make_double2(valid ? in(s, ln, r) : 0.0, 0.0); }, line);
+    col_sync<LC>();
+    run_stages<LC>(col, tl, twf);
+    col_sync<LC>();
+    cplx X[G::EPT];
+#pragma unroll
+    for (int k = 0; k < G::EPT; ++k) X[k] = col[pidx(own_pos<LC>(tl, k))];
+#pragma unroll
+    for (int f = 0; f < NOUT; ++f) {
+      col_sync<LC>();
+#pragma unroll
+      for (int k = 0; k < G::EPT; ++k) {
+        const int p = own_pos<LC>(tl, k);
+        col[pidx(brev(p, G::LOG))] = mid(s, f, p, X[k]);
+      }
+      col_sync<LC>();
+      run_stages<LC>(col, tl, twi);
+      col_sync<LC>();
+#pragma unroll
+      for (int k = 0; k < G::EPT; ++k) {
+        const int p = own_pos<LC>(tl, k);
+        const double v = col[pidx(p)].x * inv_n;  // result[i].mul(1.0/n).getReal()
+        if constexpr (NOUT == 2) {
+          if (valid) out(f, line, p, v);
+        } else {
+          acc[k] = s == 0 ? v : acc[k] + v;
+        }
+      }
+    }
+  }
+  if constexpr (NOUT == 1) {
+    if (valid) {
+#pragma unroll
+      for (int k = 0; k < G::EPT; ++k) out(0, line, own_pos<LC>(tl, k), acc[k]);
+    }
+  }
+}
+
+}  // namespace jf
+}  // namespace jw

@@ -576,7 +576,68 @@ int inverse_dispatch(const ModwtPlan& p, const double* c, double* x, long N, int
   }
 }
 
+template <int L, bool FMA>
+int level_forward(const ModwtPlan& p, int j, const double* v, long vs, double* w, long ws,
+                  double* vn, long vns, long N, int batch, hipStream_t s) {
+  const Taps t = make_taps<L>(p);
+  for (int b0 = 0; b0 < batch; b0 += 65535) {
+    const int nb = batch - b0 < 65535 ? batch - b0 : 65535;
+    dim3 grid((unsigned)((N + kNT - 1) / kNT), (unsigned)nb);
+    hipLaunchKernelGGL((modwt_fwd_level<L, FMA>), grid, dim3(kNT), 0, s, v + b0 * vs, vs,
+                       w + b0 * ws, ws, vn + b0 * vns, vns, N, 1L << (j - 1), t);
+  }
+  JW_HIP_TRY(hipGetLastError());
+  return JW_OK;
+}
+
+template <int L, bool FMA>
+int level_inverse(const ModwtPlan& p, int j, const double* v, long vs, const double* w, long ws,
+                  double* out, long os, long N, int batch, hipStream_t s) {
+  const Taps t = make_taps<L>(p);
+  for (int b0 = 0; b0 < batch; b0 += 65535) {
+    const int nb = batch - b0 < 65535 ? batch - b0 : 65535;
+    dim3 grid((unsigned)((N + kNT - 1) / kNT), (unsigned)nb);
+    hipLaunchKernelGGL((modwt_inv_level<L, FMA>), grid, dim3(kNT), 0, s, v + b0 * vs, vs,
+                       w + b0 * ws, ws, out + b0 * os, os, N, 1L << (j - 1), t);
+  }
+  JW_HIP_TRY(hipGetLastError());
+  return JW_OK;
+}
+
 }  // namespace
+
+int modwt_level_forward_device(const ModwtPlan& p, int j, const double* v, long vs, double* w,
+                               long ws, double* vn, long vns, long N, int batch, hipStream_t s) {
+  const bool fma = p.arith == JW_ARITH_FMA;
+  switch (p.L) {
+#define JW_CASE(LL)                                                                        \
+  case LL:                                                                                 \
+    return fma ? level_forward<LL, true>(p, j, v, vs, w, ws, vn, vns, N, batch, s)         \
+               : level_forward<LL, false>(p, j, v, vs, w, ws, vn, vns, N, batch, s);
+    JW_MODWT_LENGTHS(JW_CASE)
+#undef JW_CASE
+    default:
+      return fail(JW_ERR_UNSUPPORTED, "MODWT: filter length %d is not built into this library",
+                  p.L);
+  }
+}
+
+int modwt_level_inverse_device(const ModwtPlan& p, int j, const double* v, long vs,
+                               const double* w, long ws, double* out, long os, long N, int batch,
+                               hipStream_t s) {
+  const bool fma = p.arith == JW_ARITH_FMA;
+  switch (p.L) {
+#define JW_CASE(LL)                                                                        \
+  case LL:                                                                                 \
+    return fma ? level_inverse<LL, true>(p, j, v, vs, w, ws, out, os, N, batch, s)         \
+               : level_inverse<LL, false>(p, j, v, vs, w, ws, out, os, N, batch, s);
+    JW_MODWT_LENGTHS(JW_CASE)
+#undef JW_CASE
+    default:
+      return fail(JW_ERR_UNSUPPORTED, "MODWT: filter length %d is not built into this library",
+                  p.L);
+  }
+}
 
 int modwt_forward_device(const ModwtPlan& p, const double* x, double* coeffs, long n, int J,
                          int batch, hipStream_t s) {

@@ -50,7 +50,7 @@ EXPORTS = (
     "jw_fwt_plan_create", "jw_fwt_plan_destroy", "jw_fwt_forward", "jw_fwt_reverse",
     "jw_fwt2d_forward", "jw_fwt2d_reverse", "jw_fwt3d_forward", "jw_fwt3d_reverse",
     "jw_synth_uniform", "jw_cwt_fft", "jw_cwt_direct", "jw_wpt_forward", "jw_wpt_reverse",
-    "jw_fft_forward", "jw_fft_reverse", "jw_cwt_magnitude", "jw_cwt_phase", "jw_cwt_scalogram",
+    "jw_fft_forward", "jw_fft_reverse", "jw_fft_forward_ex", "jw_fft_reverse_ex", "jw_cwt_magnitude", "jw_cwt_phase", "jw_cwt_scalogram",
     "jw_cwt_fft_scalogram",
 )
 
@@ -101,6 +101,8 @@ def lib():
     L.jw_synth_uniform.argtypes = [c_dp, l, i, l, c_dp]
     L.jw_fft_forward.argtypes = [c_dp, c_dp, l, i, i, c_dp]
     L.jw_fft_reverse.argtypes = [c_dp, c_dp, l, i, i, c_dp]
+    L.jw_fft_forward_ex.argtypes = [c_dp, c_dp, l, i, i, i, c_dp]
+    L.jw_fft_reverse_ex.argtypes = [c_dp, c_dp, l, i, i, i, c_dp]
     L.jw_cwt_fft.argtypes = [i, c_dp, c_dp, l, c_dp, i, ctypes.c_double, i, c_dp, i, i, c_dp]
     L.jw_cwt_direct.argtypes = [i, c_dp, c_dp, l, c_dp, i, ctypes.c_double, i, c_dp, i, i, c_dp]
     L.jw_cwt_magnitude.argtypes = [c_dp, l, c_dp, i, c_dp]

@@ -1,7 +1,9 @@
 """FastFourierTransform host mirror (src/main/java/jwave/transforms/FastFourierTransform.java).
 
-Same names and semantics as the reference, computed by the HIP engine (jw_fft_forward /
-jw_fft_reverse):
+Same names and semantics as the reference, computed by the HIP engine (jw_fft_forward_ex /
+jw_fft_reverse_ex).  The default arithmetic is "strict": power-of-two lengths run the
+reference's own radix-2 algorithm with its recurrence twiddles (:172-212), bit for bit;
+"fma" selects the correctly rounded twiddle tables:
 * ``forward(double[])``: real input -> interleaved (re, im) spectrum of length 2n (:48-75);
 * ``reverse(double[])``: interleaved spectrum -> real part of the inverse (:83-103);
 * ``forward(Complex[])`` / ``reverse(Complex[])`` on complex arrays (:112-164), the reverse
@@ -18,7 +20,7 @@ from .. import _native
 from .._arrays import _is_torch
 
 
-def _run(fn, z):
+def _run(fn, z, arith):
     """z: complex ndarray / tensor of shape (n,) or (B, n) -> same type and shape."""
     if _is_torch(z) and z.device.type == "cuda":
         import torch
@@ -29,7 +31,7 @@ def _run(fn, z):
         batch = 1 if t.dim() == 1 else int(np.prod(t.shape[:-1]))
         stream = ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
         _native.check(fn(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(out.data_ptr()), n, batch,
-                         _native.JW_DEVICE, stream))
+                         arith, _native.JW_DEVICE, stream))
         return out
     a = np.ascontiguousarray(np.asarray(z, dtype=np.complex128))
     out = np.empty_like(a)
@@ -38,25 +40,26 @@ def _run(fn, z):
         return out
     batch = 1 if a.ndim == 1 else int(np.prod(a.shape[:-1]))
     _native.check(fn(ctypes.c_void_p(a.ctypes.data), ctypes.c_void_p(out.ctypes.data), n, batch,
-                     _native.JW_HOST, None))
+                     arith, _native.JW_HOST, None))
     return out
 
 
 class FastFourierTransform:
     """jwave.transforms.FastFourierTransform"""
 
-    def __init__(self):
+    def __init__(self, arith="strict"):
         self._name = "Fast Fourier Transform"
+        self._arith = _native.JW_ARITH_FMA if arith == "fma" else _native.JW_ARITH_STRICT
 
     def getName(self):
         return self._name
 
     # ---- Complex[] API (:112-164) ----
     def forwardComplex(self, x):
-        return _run(_native.lib().jw_fft_forward, x)
+        return _run(_native.lib().jw_fft_forward_ex, x, self._arith)
 
     def reverseComplex(self, x):
-        return _run(_native.lib().jw_fft_reverse, x)
+        return _run(_native.lib().jw_fft_reverse_ex, x, self._arith)
 
     # ---- double[] API (:48-103) ----
     def forward(self, arr):

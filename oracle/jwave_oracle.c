@@ -363,6 +363,29 @@ void jwo_modwt_inverse_fft(const double* coeffs, long N, int J, const double* g,
   modwt_inverse(coeffs, N, J, g, h, L, x, fft_conv_adj);
 }
 
+/* performConvolution with ConvolutionMethod.AUTO (:640-664): per call, FFT when the int32
+ * product signal.length * filter.length exceeds fftConvolutionThreshold, else DIRECT (the
+ * zero-skipping sums, bit-identical to circularConvolve for finite inputs). */
+static __thread int g_auto_threshold = 4096;
+static void auto_conv(const double* s, long N, const double* f, long M, int L, double* out) {
+  if (jwo_modwt_auto_uses_fft(N, M, g_auto_threshold)) fft_conv(s, N, f, M, L, out);
+  else circ_conv_nz(s, N, f, M, L, out);
+}
+static void auto_conv_adj(const double* s, long N, const double* f, long M, int L, double* out) {
+  if (jwo_modwt_auto_uses_fft(N, M, g_auto_threshold)) fft_conv_adj(s, N, f, M, L, out);
+  else circ_conv_adj_nz(s, N, f, M, L, out);
+}
+void jwo_modwt_forward_auto(const double* x, long N, int J, const double* g, const double* h,
+                            int L, int threshold, double* coeffs) {
+  g_auto_threshold = threshold;
+  modwt_forward(x, N, J, g, h, L, coeffs, auto_conv);
+}
+void jwo_modwt_inverse_auto(const double* coeffs, long N, int J, const double* g,
+                            const double* h, int L, int threshold, double* x) {
+  g_auto_threshold = threshold;
+  modwt_inverse(coeffs, N, J, g, h, L, x, auto_conv_adj);
+}
+
 /* ------------------------------------------------------------------------ */
 /* FWT: Wavelet.forward :236-260, Wavelet.reverse :277-303,                           */
 /* Haar1Orthogonal.reverse :175-207 (x0.5), FastWaveletTransform.forward/reverse :71-153 */

@@ -58,6 +58,12 @@ void jwo_modwt_forward_fft(const double* x, long N, int J, const double* g, cons
                            int L, double* coeffs);
 void jwo_modwt_inverse_fft(const double* coeffs, long N, int J, const double* g,
                            const double* h, int L, double* x);
+/* forward/inverse with ConvolutionMethod.AUTO: each convolution DIRECT or FFT by the rule below
+ * (MODWTTransform.java:640-664), as a default-constructed MODWTTransform runs them. */
+void jwo_modwt_forward_auto(const double* x, long N, int J, const double* g, const double* h,
+                            int L, int threshold, double* coeffs);
+void jwo_modwt_inverse_auto(const double* coeffs, long N, int J, const double* g,
+                            const double* h, int L, int threshold, double* x);
 /* performConvolution AUTO rule (:650-654): (int32)(N*M) > threshold, int32 wrap included. */
 int  jwo_modwt_auto_uses_fft(long N, long M, int threshold);
 

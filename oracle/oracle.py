@@ -67,21 +67,31 @@ def modwt_filters(scal, wav):
     return g, h
 
 
-def modwt_forward(x, J, g, h, method="direct"):
+def modwt_forward(x, J, g, h, method="direct", threshold=4096):
+    """method: "direct" (every up-sampled tap), "direct_nz", "fft", or "auto" (the reference's
+    per-convolution AUTO rule with fftConvolutionThreshold = threshold)."""
     x, g, h = _f64(x), _f64(g), _f64(h)
     N = x.shape[0]
     out = np.empty((J + 1, N))
+    if method == "auto":
+        lib().jwo_modwt_forward_auto(_p(x), ctypes.c_long(N), J, _p(g), _p(h), g.shape[0],
+                                     threshold, _p(out))
+        return out
     fn = {"fft": lib().jwo_modwt_forward_fft, "direct": lib().jwo_modwt_forward_direct,
           "direct_nz": lib().jwo_modwt_forward_direct_nz}[method]
     fn(_p(x), ctypes.c_long(N), J, _p(g), _p(h), g.shape[0], _p(out))
     return out
 
 
-def modwt_inverse(coeffs, g, h, method="direct"):
+def modwt_inverse(coeffs, g, h, method="direct", threshold=4096):
     c, g, h = _f64(coeffs), _f64(g), _f64(h)
     J = c.shape[0] - 1
     N = c.shape[1]
     out = np.empty(N)
+    if method == "auto":
+        lib().jwo_modwt_inverse_auto(_p(c), ctypes.c_long(N), J, _p(g), _p(h), g.shape[0],
+                                     threshold, _p(out))
+        return out
     fn = {"fft": lib().jwo_modwt_inverse_fft, "direct": lib().jwo_modwt_inverse_direct,
           "direct_nz": lib().jwo_modwt_inverse_direct_nz}[method]
     fn(_p(c), ctypes.c_long(N), J, _p(g), _p(h), g.shape[0], _p(out))

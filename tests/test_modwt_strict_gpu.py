@@ -1,0 +1,159 @@
+"""JWave's default MODWT path on the MI355X: ConvolutionMethod.AUTO (and FFT) under
+JW_ARITH_STRICT run the reference's own FFT convolution level by level
+(MODWTTransform.java:640-664, :752-837; FastFourierTransform.java:172-212), so the engine's
+values are the JVM's bit for bit -- checked against the oracle's restatement of the same path
+(oracle "auto" / "fft": recurrence twiddles, per-call filter FFT, per-level AUTO rule with the
+int32 product).  Also the JW_ARITH_STRICT FFT entry points (jw_fft_forward_ex / _reverse_ex).
+
+Bar: bit-exact (np.array_equal of the IEEE bits) for every case, including lengths where the
+rule mixes DIRECT and FFT levels and N = 2^20 (cfg2 / cfg5 geometry).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle as orc
+from _util import bits_equal, clean_signal, mse
+from jwave import FastFourierTransform, MODWTTransform
+from jwave.transforms import wavelets as W
+from jwave.transforms.modwt import ConvolutionMethod
+
+pytestmark = pytest.mark.gpu
+
+
+def ofilters(wv):
+    return orc.modwt_filters(wv.getScalingDeComposition(), wv.getWaveletDeComposition())
+
+
+def levels_fft(n, L, J, threshold=4096):
+    return [orc.auto_uses_fft(n, (L - 1) * (1 << (j - 1)) + 1, threshold) for j in range(1, J + 1)]
+
+
+# (wavelet, n, J, threshold): one-column lengths (n <= 4096), the two-pass column path
+# (n >= 8192), mixed DIRECT/FFT levels, multi-wrap filters (sym8 on n = 8), all-DIRECT and
+# all-FFT thresholds
+AUTO_CASES = [
+    ("Haar1", 8, 3, 4096), ("Haar1", 4096, 12, 4096), ("Daubechies4", 64, 6, 4096),
+    ("Daubechies4", 512, 4, 4096), ("Daubechies4", 512, 1, 4096), ("Symlet8", 8, 3, 4096),
+    ("Symlet8", 512, 6, 4096), ("Daubechies4", 4096, 8, 4096), ("Daubechies4", 8192, 8, 4096),
+    ("Daubechies8", 1 << 15, 7, 4096), ("Coiflet5", 2048, 5, 4096), ("Daubechies2", 16, 4, 4096),
+    ("Daubechies4", 1 << 14, 6, (1 << 14) * 30), ("Daubechies4", 256, 3, -1),
+    ("Daubechies4", 4096, 5, 2**31 - 1), ("Symlet8", 1 << 13, 6, 4096),
+    ("Daubechies20", 1024, 6, 4096), ("Haar1", 2, 1, -1), ("Daubechies4", 4, 2, -1),
+]
+
+
+@pytest.mark.parametrize("wname,n,J,threshold", AUTO_CASES)
+def test_auto_bit_exact_vs_reference_path(wname, n, J, threshold):
+    wv = W.by_name(wname)
+    g, h = ofilters(wv)
+    xs = np.stack([orc.fill_uniform(n, 11 + n + b) for b in range(3)])
+    m = MODWTTransform(wv, fftThreshold=threshold)  # AUTO, JW_ARITH_STRICT: the defaults
+    c = m.forwardMODWT(xs, J)
+    for b in range(3):
+        assert bits_equal(c[b], orc.modwt_forward(xs[b], J, g, h, "auto", threshold)), b
+    xr = m.inverseMODWT(c)
+    for b in range(3):
+        assert bits_equal(xr[b], orc.modwt_inverse(c[b], g, h, "auto", threshold)), b
+    # the reference's own reconstruction bar (MODWTInverseTest.java:17-232, MSE < 1e-10)
+    assert mse(xr, xs) < 1e-10
+
+
+@pytest.mark.parametrize("wname,n,J", [("Daubechies4", 128, 3), ("Symlet8", 8, 3),
+                                       ("Haar1", 256, 4), ("Daubechies6", 1 << 13, 5),
+                                       ("Symlet8", 1 << 16, 6)])
+def test_fft_method_bit_exact(wname, n, J):
+    # setConvolutionMethod(FFT): every level through circularConvolveFFT (:752-837)
+    wv = W.by_name(wname)
+    g, h = ofilters(wv)
+    x = clean_signal(n) + orc.fill_uniform(n, n)
+    m = MODWTTransform(wv)
+    m.setConvolutionMethod(ConvolutionMethod.FFT)
+    c = m.forwardMODWT(x, J)
+    assert bits_equal(c, orc.modwt_forward(x, J, g, h, "fft"))
+    assert bits_equal(m.inverseMODWT(c), orc.modwt_inverse(c, g, h, "fft"))
+
+
+def test_mixed_levels_keep_direct_levels_exact():
+    # db4, n = 512: level 1 has N*M = 512*8 = 4096, not > 4096 -> DIRECT in the reference; the
+    # other levels take the FFT path.  Level 1's row is the DIRECT value, bit for bit.
+    wv = W.Daubechies4()
+    g, h = ofilters(wv)
+    x = orc.fill_uniform(512, 9)
+    assert levels_fft(512, 8, 4) == [False, True, True, True]
+    c = MODWTTransform(wv).forwardMODWT(x, 4)
+    assert bits_equal(c[0], orc.modwt_forward(x, 1, g, h, "direct_nz")[0])
+    assert not bits_equal(c[1], orc.modwt_forward(x, 4, g, h, "direct_nz")[1])
+
+
+@pytest.mark.parametrize("wname,J", [("Daubechies4", 8), ("Symlet8", 6), ("Daubechies4", 10)])
+def test_auto_full_size(wname, J, device):
+    # cfg2 / cfg5 geometry through JWave's default path.  db4 J=10: level 10's N*M product
+    # wraps negative in int32 (:653), so the reference -- and the engine -- run it DIRECT
+    # between FFT levels.
+    import torch
+    from jwave import _native
+    wv = W.by_name(wname)
+    g, h = ofilters(wv)
+    B, n = 2, 1 << 20
+    if J == 10:
+        assert levels_fft(n, wv.getMotherWavelength(), J)[-1] is False
+    x = torch.empty((B, n), dtype=torch.float64, device=device)
+    _native.check(_native.lib().jw_synth_uniform(ctypes.c_void_p(x.data_ptr()), n, B, 42, None))
+    m = MODWTTransform(wv)
+    c = m.forwardMODWT(x, J)
+    xr = m.inverseMODWT(c)
+    torch.cuda.synchronize()
+    x1 = orc.fill_uniform(n, 43)
+    got = c[1].cpu().numpy()
+    ref = orc.modwt_forward(x1, J, g, h, "auto")
+    assert bits_equal(got, ref)
+    assert bits_equal(xr[1].cpu().numpy(), orc.modwt_inverse(ref, g, h, "auto"))
+    # JWave's FFT path reconstructs to ~4e-10 here: the engine's is the same
+    assert (xr - x).abs().max().item() < 1e-8
+
+
+POW2 = [2, 4, 8, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 1 << 14, 1 << 15, 1 << 16,
+        1 << 17, 1 << 18, 1 << 19, 1 << 20, 1 << 21]
+
+
+@pytest.mark.parametrize("n", POW2)
+def test_fft_strict_bit_exact(n):
+    rng = np.random.default_rng(n)
+    B = 3 if n <= (1 << 18) else 1
+    z = rng.uniform(-1, 1, (B, n)) + 1j * rng.uniform(-1, 1, (B, n))
+    f = FastFourierTransform()  # arith="strict" is the default
+    X = f.forwardComplex(z)
+    for b in range(B):
+        assert bits_equal(X[b].view(np.float64), orc.fft(z[b]).view(np.float64))
+    zr = f.reverseComplex(X)
+    for b in range(B):
+        assert bits_equal(zr[b].view(np.float64), orc.fft(X[b], inverse=True).view(np.float64))
+
+
+def test_fft_strict_in_place_and_device(device):
+    import torch
+    from jwave import _native
+    n, B = 1 << 14, 4
+    rng = np.random.default_rng(5)
+    z = rng.uniform(-1, 1, (B, n)) + 1j * rng.uniform(-1, 1, (B, n))
+    t = torch.from_numpy(z).to(device)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    _native.check(_native.lib().jw_fft_forward_ex(ctypes.c_void_p(t.data_ptr()),
+                                                  ctypes.c_void_p(t.data_ptr()), n, B,
+                                                  _native.JW_ARITH_STRICT, _native.JW_DEVICE,
+                                                  stream))
+    torch.cuda.synchronize()
+    got = t.cpu().numpy()
+    for b in range(B):
+        assert bits_equal(got[b].view(np.float64), orc.fft(z[b]).view(np.float64))
+
+
+def test_fft_strict_largest_column():
+    # 2^24 = 4096 x 4096: the 4096-point column kernels (the chirp-z size of n up to 2^23)
+    n = 1 << 24
+    rng = np.random.default_rng(24)
+    z = rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n)
+    X = FastFourierTransform().forwardComplex(z)
+    assert bits_equal(X.view(np.float64), orc.fft(z).view(np.float64))
