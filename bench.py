@@ -139,6 +139,13 @@ def parse():
     return ap.parse_args()
 
 
+CORES_REASON = ("threads = OMP_NUM_THREADS when set: the GPU box allots each GPU a share of 16 "
+                "host CPUs (OMP_NUM_THREADS=16 there) although affinity shows the whole "
+                "machine; BASELINE.md's 'all host cores' would oversubscribe the other GPUs' "
+                "shares, so the baseline is stated per 16-CPU share (scale by affinity_cpus/16 "
+                "for a whole-host estimate)")
+
+
 def cpu_baseline(wname, n, J):
     """Oracle (C restatement of JWave's CPU path) on a bounded sample, signals split by
     ForkJoin-style recursive halving (ParallelTransform.java:222-335)."""
@@ -169,6 +176,7 @@ def cpu_baseline(wname, n, J):
                    f"(FFT convolution, MODWTTransform.java:653), ForkJoin halving over signals on "
                    f"{threads} threads: {t_auto:.2f} s; DIRECT-faithful on {threads} x N={nd}: "
                    f"{threads * nd / t_direct / 1e6:.3f} Msamples/s"),
+        "cores_reason": CORES_REASON,
         "direct_value": threads * nd / t_direct / 1e6,
     }, **host)
 
@@ -244,7 +252,7 @@ def main_cwt(args, dev, rank, world):
                     "sample": f"{nsig} signals x N={n}, {ns} scales, oracle transformFFTParallel "
                               f"(scales in parallel per signal, signals in the outer pool, "
                               f"recurrence-twiddle radix-2 FFT like FastFourierTransform.java), "
-                              f"{threads} threads: {tc:.2f} s"}, **host)
+                              f"{threads} threads: {tc:.2f} s", "cores_reason": CORES_REASON}, **host)
     if rank == 0:
         ach = per_call / (ms * 1e-3) / 1e9
         print(json.dumps({
@@ -353,7 +361,7 @@ def main_fwt2d(args, dev, rank, world):
                     "kind": "port",
                     "sample": f"{nimg} images {R}x{R} Daubechies8 12x12 levels forward+reverse, "
                               f"oracle ParallelTransform pattern (rows task -> columns task) on "
-                              f"{threads} threads: {tc:.2f} s"}, **host)
+                              f"{threads} threads: {tc:.2f} s", "cores_reason": CORES_REASON}, **host)
     if rank == 0:
         per = 64 * B * R * R  # 2 passes x (read + write) x 8 B, forward + reverse
         ach = per / ((fms + rms_) * 1e-3) / 1e9
@@ -499,26 +507,29 @@ def main():
         return f"normwise {float(np.max(np.abs(got - ref)) / np.max(np.abs(ref))):.2e}"
 
     def extra_paths(nb=16, reps=3):
-        """Two secondary figures on a 16-signal sub-batch (not the headline):
+        """Secondary figures on a 16-signal sub-batch (never the headline):
         * JW_HOST: host double[] in, host double[] out -- what a JNI caller passing Java arrays
-          gets, PCIe staging included (pinned bounce buffers, cached HBM staging);
-        * AUTO: the reference's default ConvolutionMethod, which at this N takes the FFT path
-          (MODWTTransform.java:653); deviation of its coefficients from the oracle's restatement
-          of the reference's FFT path and from the exact DIRECT oracle (one signal)."""
+          gets, PCIe staging included;
+        * AUTO under JW_ARITH_STRICT: the reference's default ConvolutionMethod, which at this N
+          takes the FFT path at every level (MODWTTransform.java:653), run as the reference runs
+          it (its own FFT, level by level): bit-exactness against the oracle's restatement of
+          that path (one signal) and throughput;
+        * FFT under JW_ARITH_FMA: the exact-twiddle frequency-domain pyramid (the fast FFT
+          option) and its deviation from the reference's FFT path and from DIRECT."""
         import numpy as np
         import oracle as orc
         P = lambda a: ctypes.c_void_p(a.ctypes.data if isinstance(a, np.ndarray)  # noqa: E731
                                       else a.data_ptr())
-        m = MODWTTransform(wv, arith=args.arith)  # AUTO, fftThreshold 4096
-        plan = m.initializeFilterCache()
         xh = np.ascontiguousarray(x[:nb].cpu().numpy())
         ch = np.empty((nb, J + 1, n))
         xrh = np.empty((nb, n))
+        hxf = MODWTTransform(wv, arith=args.arith)  # owns its plan: keep it referenced
+        hplan = hxf.initializeFilterCache()
 
         def host_step():
-            _native.check(lib.jw_modwt_forward(plan, P(xh), P(ch), n, J, nb, _native.JW_CONV_DIRECT,
+            _native.check(lib.jw_modwt_forward(hplan, P(xh), P(ch), n, J, nb, _native.JW_CONV_DIRECT,
                                                _native.JW_HOST, None))
-            _native.check(lib.jw_modwt_inverse(plan, P(ch), P(xrh), n, J, nb, _native.JW_CONV_DIRECT,
+            _native.check(lib.jw_modwt_inverse(hplan, P(ch), P(xrh), n, J, nb, _native.JW_CONV_DIRECT,
                                                _native.JW_HOST, None))
 
         host_step()  # the staging buffers grow once
@@ -534,31 +545,47 @@ def main():
         ca = torch.empty((nb, J + 1, n), dtype=torch.float64, device=dev)
         xra = torch.empty((nb, n), dtype=torch.float64, device=dev)
 
-        def auto_step():
-            _native.check(lib.jw_modwt_forward(plan, P(x), P(ca), n, J, nb, _native.JW_CONV_AUTO,
-                                               _native.JW_DEVICE, sptr))
-            _native.check(lib.jw_modwt_inverse(plan, P(ca), P(xra), n, J, nb, _native.JW_CONV_AUTO,
-                                               _native.JW_DEVICE, sptr))
+        def timed(arith, method):
+            xf = MODWTTransform(wv, arith=arith)  # owns its plan: keep it referenced
+            plan = xf.initializeFilterCache()
 
-        auto_step()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            auto_step()
-        torch.cuda.synchronize()
-        ta = (time.perf_counter() - t0) / reps
+            def step():
+                _native.check(lib.jw_modwt_forward(plan, P(x), P(ca), n, J, nb, method,
+                                                   _native.JW_DEVICE, sptr))
+                _native.check(lib.jw_modwt_inverse(plan, P(ca), P(xra), n, J, nb, method,
+                                                   _native.JW_DEVICE, sptr))
+            step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                step()
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t0) / reps
+
         g, h = orc.modwt_filters(wv.getScalingDeComposition(), wv.getWaveletDeComposition())
-        got = ca[0].cpu().numpy()
-        jw_fft = orc.modwt_forward(xh[0], J, g, h, "fft")
+        jw_auto = orc.modwt_forward(xh[0], J, g, h, "auto")  # = "fft" wherever N*M_j > 4096
         exact = orc.modwt_forward(xh[0], J, g, h, "direct_nz")
         dev_rows = lambda a, b: max(float(np.max(np.abs(a[r] - b[r])) / np.max(np.abs(b[r])))  # noqa: E731
                                     for r in range(J + 1))
-        auto = {"method": "AUTO -> FFT (N*M_j > 4096 at every level, MODWTTransform.java:653)",
+        ta = timed("strict", _native.JW_CONV_AUTO)
+        got = ca[0].cpu().numpy()
+        auto = {"method": "AUTO, JW_ARITH_STRICT (JWave's default): every level whose N*M_j > 4096 "
+                          "(MODWTTransform.java:653) through the reference's own FFT convolution",
                 "value": round(nb * n / ta / 1e6, 1), "unit": "Msamples/s", "signals": nb,
-                "max_row_normwise_vs_reference_fft_path": dev_rows(got, jw_fft),
-                "max_row_normwise_vs_exact_direct": dev_rows(got, exact),
-                "reference_fft_path_vs_exact_direct": dev_rows(jw_fft, exact),
+                "ms_per_signal_fwd_inv": round(ta * 1e3 / nb, 3),
+                "bit_exact_vs_reference_path": bool(np.array_equal(got.view(np.uint64),
+                                                                   jw_auto.view(np.uint64))),
+                "max_abs_vs_reference_path": float(np.max(np.abs(got - jw_auto))),
+                "reference_path_vs_exact_direct": dev_rows(jw_auto, exact),
                 "recon_max_abs": (xra - x[:nb]).abs().max().item()}
+        tp = timed("fma", _native.JW_CONV_FFT)
+        got = ca[0].cpu().numpy()
+        auto["fft_pyramid_fma"] = {
+            "method": "FFT, JW_ARITH_FMA: exact-twiddle frequency-domain pyramid (fast option)",
+            "value": round(nb * n / tp / 1e6, 1), "unit": "Msamples/s",
+            "max_row_normwise_vs_reference_fft_path": dev_rows(got, jw_auto),
+            "max_row_normwise_vs_exact_direct": dev_rows(got, exact),
+            "recon_max_abs": (xra - x[:nb]).abs().max().item()}
         return host, auto
 
     alt_arith = "strict" if args.arith == "fma" else "fma"

@@ -12,8 +12,19 @@
  *   JW_ERR_FAILURE          -> jwave.exceptions.JWaveFailure      (checked)
  *
  * Threading: plans are immutable after creation and may be shared by any number of host
- * threads (the reference's MODWTThreadSafetyTest pattern).  Every call is reentrant; the
- * only global state is a thread-local error message.
+ * threads (the reference's MODWTThreadSafetyTest pattern).  Every call is reentrant.
+ * Process-wide state, all internally synchronised:
+ *   - a thread-local error message (jw_last_error) and the calling thread's current device
+ *     (jw_set_device; HIP's own per-thread device);
+ *   - per-device caches of tables that depend on sizes / filters only (FFT twiddles, chirp-z
+ *     tables, MODWT filter spectra and pair tables), each within a byte budget (a call past
+ *     the budget builds its own), built once per key (the first call for a key synchronises
+ *     its stream once) and freed by jw_release_caches();
+ *   - one private stream-ordered memory pool per device for workspaces (the device's default
+ *     pool is never touched); it keeps freed memory for reuse, gives it back when an
+ *     allocation would fail, and on jw_release_caches();
+ *   - per host thread and device, a non-blocking stream and two 32 MiB pinned bounce buffers
+ *     for JW_HOST staging.
  */
 #ifndef JWAVE_HIP_H
 #define JWAVE_HIP_H
@@ -50,6 +61,23 @@ const char* jw_last_error(void);
 /* Library version string and the gfx target it was built for. */
 const char* jw_version(void);
 
+/* ---- devices (one process may drive several GPUs, e.g. a JVM whose ForkJoin workers fan out
+ * as ParallelTransform.java:83-86 / ContinuousWaveletTransform.java:511-565 do) ---- */
+/* Number of visible HIP devices (0 when none; never an error). */
+int jw_device_count(int* count);
+/* Make `ordinal` the calling thread's device: every later call of this thread runs there, its
+ * JW_DEVICE pointers must live there, and the caches are kept per device.  Invalid ordinals ->
+ * JW_ERR_ILLEGAL_ARGUMENT ("device ordinal must be >= 0", "... out of range: k HIP device(s)
+ * visible"). */
+int jw_set_device(int ordinal);
+int jw_get_device(int* ordinal);
+/* MODWTTransform.clearFilterCache (:556) for the device side: frees every cached table (FFT
+ * twiddles, chirp-z tables, MODWT filter spectra / pair tables) on every device the library has
+ * run on and returns the memory pools' unused workspace memory to the driver.  Waits for calls
+ * in flight (and the kernels they queued) before freeing; later calls rebuild what they need.
+ * Returns the bytes of tables freed (>= 0). */
+long jw_release_caches(void);
+
 /* ======================================================================
  * MODWT  (replaces MODWTTransform.forwardMODWT :256 / inverseMODWT :337)
  * ====================================================================== */
@@ -69,13 +97,21 @@ int jw_modwt_plan_filters(const jw_modwt_plan* plan, double* g, double* h);
  * x: batch x n.  coeffs: batch x (levels+1) x n = [W_1..W_J, V_J] per signal.
  * Validation order and messages follow MODWTTransform.java:257-282; n == 0 is a no-op.
  * method: JW_CONV_* (the Java object's setConvolutionMethod state, passed per call).
- * JW_CONV_FFT with 2 <= n <= 2^23 runs the FFT-convolution path (MODWTTransform.java
- * :752-837: results within 1e-10 of DIRECT; non-power-of-two n through a chirp-z transform,
- * as FastFourierTransform.java:259-324 does); AUTO, DIRECT, and FFT at other n run the
- * direct kernels, which are bit-identical to the JVM's DIRECT path. */
+ * With a JW_ARITH_STRICT plan (the JVM's arithmetic) every level takes the convolution the
+ * reference's performConvolution takes (:640-664): FFT always, DIRECT never, AUTO when the
+ * int32 product n * M_j > fftConvolutionThreshold (M_j = (L-1) 2^(j-1) + 1, wrap included).
+ * DIRECT levels are bit-identical to circularConvolve (:677-690).  FFT levels run the
+ * reference's circularConvolveFFT (:752-786) with its own FFT (FastFourierTransform.java
+ * :172-212), bit-identical to the JVM for power-of-two 2 <= n <= 2^23; other n run the
+ * exact-twiddle chirp-z pyramid (within 1e-10 of DIRECT).
+ * With a JW_ARITH_FMA plan (the fast contract) FFT runs the exact-twiddle frequency-domain
+ * pyramid for 2 <= n <= 2^23 (within 1e-10 of DIRECT); AUTO and DIRECT run the direct kernels
+ * (faster and more accurate than any FFT path on this engine). */
 int jw_modwt_forward(const jw_modwt_plan* plan, const double* x, double* coeffs, long n,
                      int levels, int batch, int method, int where, void* stream);
-/* inverseMODWT(coefficients) (:337-375): coeffs batch x (levels+1) x n -> x batch x n. */
+/* inverseMODWT(coefficients) (:337-375): coeffs batch x (levels+1) x n -> x batch x n.
+ * Method and arithmetic as jw_modwt_forward (circularConvolveAdjoint :703-716,
+ * circularConvolveFFTAdjoint :798-837). */
 int jw_modwt_inverse(const jw_modwt_plan* plan, const double* coeffs, double* x, long n,
                      int levels, int batch, int method, int where, void* stream);
 

@@ -24,16 +24,27 @@ public class HipContinuousWaveletTransform extends ContinuousWaveletTransform {
   private final ContinuousWavelet wavelet;
   private final int padding; // PaddingType.ordinal(): the reference keeps it private (:84)
   private final int arith;
+  private final int device; // -1: the calling thread's current device
 
   public HipContinuousWaveletTransform(ContinuousWavelet w) {
     this(w, PaddingType.ZERO, HipMODWTTransform.ARITH_STRICT);
   }
 
   public HipContinuousWaveletTransform(ContinuousWavelet w, PaddingType p, int arith) {
+    this(w, p, arith, -1);
+  }
+
+  /** On GPU {@code device} (jw_set_device before every native call of the calling thread). */
+  public HipContinuousWaveletTransform(ContinuousWavelet w, PaddingType p, int arith, int device) {
     super(w, p);
     wavelet = w;
     padding = p.ordinal();
     this.arith = arith;
+    this.device = device;
+  }
+
+  private void onDevice() {
+    if (device >= 0) HipEngine.setDevice(device);
   }
 
   /** JW_CWT_* kind, or -1 when the engine has no kernel for this wavelet class. */
@@ -75,6 +86,7 @@ public class HipContinuousWaveletTransform extends ContinuousWaveletTransform {
   public CWTResult transformFFT(double[] signal, double[] scales, double samplingRate) {
     int k = kind();
     if (k < 0) return super.transformFFT(signal, scales, samplingRate);
+    onDevice();
     double[][] rows = nTransformFFT(k, params(), signal, scales, samplingRate, padding);
     return result(rows, scales, signal.length, samplingRate);
   }
@@ -86,6 +98,7 @@ public class HipContinuousWaveletTransform extends ContinuousWaveletTransform {
   public double[] transformFFTScalogram(double[] signal, double[] scales, double samplingRate) {
     int k = kind();
     if (k < 0) return super.transformFFT(signal, scales, samplingRate).getScalogram();
+    onDevice();
     return nScalogramFFT(k, params(), signal, scales, samplingRate, padding);
   }
 
@@ -98,6 +111,7 @@ public class HipContinuousWaveletTransform extends ContinuousWaveletTransform {
   public CWTResult transform(double[] signal, double[] scales, double samplingRate) {
     int k = kind();
     if (k < 0) return super.transform(signal, scales, samplingRate);
+    onDevice();
     double[][] rows = nTransformDirect(k, params(), signal, scales, samplingRate, arith);
     return result(rows, scales, signal.length, samplingRate);
   }

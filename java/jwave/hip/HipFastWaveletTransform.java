@@ -1,5 +1,8 @@
 package jwave.hip;
 
+import java.lang.ref.Cleaner;
+import java.lang.ref.Reference;
+
 import jwave.exceptions.JWaveException;
 import jwave.transforms.FastWaveletTransform;
 import jwave.transforms.wavelets.Wavelet;
@@ -10,6 +13,10 @@ import jwave.transforms.wavelets.haar.Haar1Orthogonal;
  * and the 2-D row/column transform (BasicTransform.java:361-474) on the MI355X, bit-identical
  * to the JVM with ARITH_STRICT.  Messages and exception classes are the reference's
  * ("given array length is not 2^p ...", "given level is out of range for given array").
+ *
+ * <p>The native plan is freed by a {@link Cleaner} once the transform is unreachable; every
+ * native call keeps the transform reachable until it returns (reachabilityFence), so the plan
+ * cannot be freed under a running call.
  */
 public class HipFastWaveletTransform extends FastWaveletTransform {
   static {
@@ -19,46 +26,63 @@ public class HipFastWaveletTransform extends FastWaveletTransform {
   public static final int ARITH_STRICT = 0, ARITH_FMA = 1;
   private static final int KIND_GENERIC = 0, KIND_HAAR_ORTH = 1; // JW_WAVELET_*
 
+  private static final Cleaner CLEANER = Cleaner.create();
+
   private final long plan; // immutable; lives as long as the transform
+  private final int device; // -1: the calling thread's current device
 
-  public HipFastWaveletTransform(Wavelet w) { this(w, ARITH_STRICT); }
+  public HipFastWaveletTransform(Wavelet w) { this(w, ARITH_STRICT, -1); }
 
-  public HipFastWaveletTransform(Wavelet w, int arith) {
+  public HipFastWaveletTransform(Wavelet w, int arith) { this(w, arith, -1); }
+
+  public HipFastWaveletTransform(Wavelet w, int arith, int device) {
     super(w);
-    plan = nPlanCreate(w.getScalingDeComposition(), w.getWaveletDeComposition(),
-                       w.getScalingReConstruction(), w.getWaveletReConstruction(),
-                       w.getMotherWavelength(), w.getTransformWavelength(),
-                       // Haar1Orthogonal overrides reverse (Haar1Orthogonal.java:175-207)
-                       w instanceof Haar1Orthogonal ? KIND_HAAR_ORTH : KIND_GENERIC, arith);
+    this.device = device;
+    final long p = nPlanCreate(w.getScalingDeComposition(), w.getWaveletDeComposition(),
+                               w.getScalingReConstruction(), w.getWaveletReConstruction(),
+                               w.getMotherWavelength(), w.getTransformWavelength(),
+                               // Haar1Orthogonal overrides reverse (Haar1Orthogonal.java:175-207)
+                               w instanceof Haar1Orthogonal ? KIND_HAAR_ORTH : KIND_GENERIC, arith);
+    plan = p;
+    CLEANER.register(this, () -> nPlanDestroy(p)); // the action must not capture this
+  }
+
+  private double[] line(int op, double[] x, int level) throws JWaveException {
+    try {
+      if (device >= 0) HipEngine.setDevice(device);
+      return nLine(plan, op, x, level);
+    } finally {
+      Reference.reachabilityFence(this);
+    }
+  }
+
+  private double[][] matrix(int op, double[][] x, int lvlM, int lvlN) throws JWaveException {
+    try {
+      if (device >= 0) HipEngine.setDevice(device);
+      return nMatrix(plan, op, x, lvlM, lvlN);
+    } finally {
+      Reference.reachabilityFence(this);
+    }
   }
 
   @Override
   public double[] forward(double[] arrTime, int level) throws JWaveException {
-    return nLine(plan, 0, arrTime, level);
+    return line(0, arrTime, level);
   }
 
   @Override
   public double[] reverse(double[] arrHilb, int level) throws JWaveException {
-    return nLine(plan, 1, arrHilb, level);
+    return line(1, arrHilb, level);
   }
 
   @Override
   public double[][] forward(double[][] matTime, int lvlM, int lvlN) throws JWaveException {
-    return nMatrix(plan, 0, matTime, lvlM, lvlN);
+    return matrix(0, matTime, lvlM, lvlN);
   }
 
   @Override
   public double[][] reverse(double[][] matFreq, int lvlM, int lvlN) throws JWaveException {
-    return nMatrix(plan, 1, matFreq, lvlM, lvlN);
-  }
-
-  @Override
-  protected void finalize() throws Throwable {
-    try {
-      nPlanDestroy(plan);
-    } finally {
-      super.finalize();
-    }
+    return matrix(1, matFreq, lvlM, lvlN);
   }
 
   static native long nPlanCreate(double[] sD, double[] wD, double[] sR, double[] wR,

@@ -1,6 +1,7 @@
 package jwave.hip;
 
 import java.nio.ByteBuffer;
+import java.nio.ByteOrder;
 import java.util.concurrent.atomic.AtomicInteger;
 
 import jwave.transforms.MODWTTransform;
@@ -25,6 +26,7 @@ public class HipMODWTTransform extends MODWTTransform {
   public static final int ARITH_STRICT = 0, ARITH_FMA = 1;
 
   private final int arith;
+  private final int device; // -1: the calling thread's current device
   private final Object planLock = new Object();
   private Plan plan; // guarded by planLock
 
@@ -45,14 +47,20 @@ public class HipMODWTTransform extends MODWTTransform {
   public HipMODWTTransform(Wavelet w, int arith) {
     super(w);
     this.arith = arith;
+    this.device = -1;
   }
 
-  public HipMODWTTransform(Wavelet w, int fftThreshold, int arith) {
+  public HipMODWTTransform(Wavelet w, int fftThreshold, int arith) { this(w, fftThreshold, arith, -1); }
+
+  /** On GPU {@code device} (jw_set_device before every native call of the calling thread). */
+  public HipMODWTTransform(Wavelet w, int fftThreshold, int arith, int device) {
     super(w, fftThreshold); // MODWTTransform.java:191
     this.arith = arith;
+    this.device = device;
   }
 
   private Plan acquire() {
+    if (device >= 0) HipEngine.setDevice(device);
     synchronized (planLock) {
       if (plan == null) {
         Wavelet w = getWavelet();
@@ -92,6 +100,7 @@ public class HipMODWTTransform extends MODWTTransform {
    * whole batch.
    */
   public void forwardMODWT(ByteBuffer x, ByteBuffer coeffs, int n, int maxLevel, int batch) {
+    checkDirect(x, coeffs);
     Plan p = acquire();
     try {
       nForwardDirect(p.handle, x, coeffs, n, maxLevel, batch, getConvolutionMethod().ordinal());
@@ -102,11 +111,21 @@ public class HipMODWTTransform extends MODWTTransform {
 
   /** Batched inverse over direct buffers: coeffs batch x (levels+1) x n -> x batch x n. */
   public void inverseMODWT(ByteBuffer coeffs, ByteBuffer x, int n, int levels, int batch) {
+    checkDirect(coeffs, x);
     Plan p = acquire();
     try {
       nInverseDirect(p.handle, coeffs, x, n, levels, batch, getConvolutionMethod().ordinal());
     } finally {
       p.release();
+    }
+  }
+
+  /** The engine reads direct buffers from their base address in native byte order. */
+  private static void checkDirect(ByteBuffer a, ByteBuffer b) {
+    for (ByteBuffer buf : new ByteBuffer[] {a, b}) {
+      if (!buf.isDirect() || buf.position() != 0 || buf.order() != ByteOrder.nativeOrder())
+        throw new IllegalArgumentException(
+            "direct ByteBuffers at position 0 in native byte order required");
     }
   }
 
@@ -119,6 +138,7 @@ public class HipMODWTTransform extends MODWTTransform {
         plan = null;
       }
     }
+    HipEngine.releaseCaches(); // the device-side tables (filter spectra, FFT twiddles)
   }
 
   private static native long nPlanCreate(double[] scalDec, double[] wavDec, int fftThreshold,

@@ -16,6 +16,7 @@
  *    them only after in-flight calls finish (a reference count, see HipMODWTTransform). */
 #include <jni.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 
 #include "jwave_hip.h"
@@ -63,12 +64,23 @@ static jobjectArray rows_out(JNIEnv* env, const double* c, jsize rows, jsize n) 
   return out;
 }
 
-/* double[rows][n] -> rows x n doubles; every row must have length n */
+static void iae(JNIEnv* env, const char* msg) {
+  jclass c = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
+  if (c) (*env)->ThrowNew(env, c, msg);
+}
+
+/* double[rows][n] -> rows x n doubles; every row must have length n.  An empty outer array
+ * gives rows = n = 0 and a 1-element buffer (the engine treats n == 0 as a no-op). */
 static double* rows_in(JNIEnv* env, jobjectArray a, jsize* rows_out_, jsize* n_out) {
-  const jsize R = (*env)->GetArrayLength(env, a);
-  jdoubleArray r0 = (jdoubleArray)(*env)->GetObjectArrayElement(env, a, 0);
-  const jsize n = r0 ? (*env)->GetArrayLength(env, r0) : 0;
-  double* c = malloc(sizeof(double) * (size_t)R * (n ? n : 1));
+  const jsize R = a ? (*env)->GetArrayLength(env, a) : 0;
+  jsize n = 0;
+  if (R > 0) {
+    jdoubleArray r0 = (jdoubleArray)(*env)->GetObjectArrayElement(env, a, 0);
+    if ((*env)->ExceptionCheck(env)) return NULL;
+    n = r0 ? (*env)->GetArrayLength(env, r0) : 0;
+    if (r0) (*env)->DeleteLocalRef(env, r0);
+  }
+  double* c = malloc(sizeof(double) * (size_t)(R ? R : 1) * (n ? n : 1));
   if (!c) {
     oom(env);
     return NULL;
@@ -89,10 +101,52 @@ static double* rows_in(JNIEnv* env, jobjectArray a, jsize* rows_out_, jsize* n_o
   return c;
 }
 
+/* Direct NIO buffer of at least `doubles` doubles (capacity in bytes), or NULL with an
+ * IllegalArgumentException pending.  The buffer's position is ignored (the engine reads from
+ * its base address) and its contents must be in native byte order: HipMODWTTransform checks
+ * both on the Java side. */
+static void* direct_buffer(JNIEnv* env, jobject buf, long long doubles, const char* what) {
+  void* p = buf ? (*env)->GetDirectBufferAddress(env, buf) : NULL;
+  if (!p) {
+    iae(env, "direct ByteBuffers required");
+    return NULL;
+  }
+  const jlong cap = (*env)->GetDirectBufferCapacity(env, buf);
+  if (cap < 0 || (long long)cap / (long long)sizeof(double) < doubles) {
+    char msg[160];
+    snprintf(msg, sizeof msg, "%s buffer holds %lld bytes, %lld doubles needed", what,
+             (long long)cap, doubles);
+    iae(env, msg);
+    return NULL;
+  }
+  return p;
+}
+
 /* ---------------------------------------------------------------- device selection */
 JNIEXPORT jstring JNICALL Java_jwave_hip_HipEngine_nVersion(JNIEnv* env, jclass cls) {
   (void)cls;
   return (*env)->NewStringUTF(env, jw_version());
+}
+
+/* jw_set_device for the calling thread (every transform with a device ordinal calls it before
+ * its native call, on the same thread) */
+JNIEXPORT void JNICALL Java_jwave_hip_HipEngine_nSetDevice(JNIEnv* env, jclass cls, jint ordinal) {
+  (void)cls;
+  const int st = jw_set_device(ordinal);
+  if (st != JW_OK) jw_throw(env, st);
+}
+
+JNIEXPORT jint JNICALL Java_jwave_hip_HipEngine_nDeviceCount(JNIEnv* env, jclass cls) {
+  (void)env, (void)cls;
+  int n = 0;
+  (void)jw_device_count(&n);
+  return n;
+}
+
+/* MODWTTransform.clearFilterCache's device side: every cached table (jw_release_caches) */
+JNIEXPORT jlong JNICALL Java_jwave_hip_HipEngine_nReleaseCaches(JNIEnv* env, jclass cls) {
+  (void)env, (void)cls;
+  return (jlong)jw_release_caches();
 }
 
 /* ---------------------------------------------------------------- MODWT */
@@ -176,18 +230,25 @@ JNIEXPORT jdoubleArray JNICALL Java_jwave_hip_HipMODWTTransform_nInverse(JNIEnv*
 }
 
 /* Batched forward/inverse over direct NIO buffers (no copies on the JVM side):
- * x: batch*n doubles, coeffs: batch*(J+1)*n doubles, native byte order. */
+ * x: batch*n doubles, coeffs: batch*(J+1)*n doubles, native byte order, position ignored.
+ * Sizes are checked against the buffers' capacities before the engine touches them. */
+static int direct_sizes_ok(JNIEnv* env, jlong n, jint J, jint batch) {
+  if (n < 0 || J < 0 || batch < 0) {
+    iae(env, "n, levels and batch must not be negative");
+    return 0;
+  }
+  return 1;
+}
+
 JNIEXPORT void JNICALL Java_jwave_hip_HipMODWTTransform_nForwardDirect(
     JNIEnv* env, jclass cls, jlong plan, jobject xbuf, jobject cbuf, jlong n, jint J, jint batch,
     jint method) {
   (void)cls;
-  const double* x = (const double*)(*env)->GetDirectBufferAddress(env, xbuf);
-  double* c = (double*)(*env)->GetDirectBufferAddress(env, cbuf);
-  if (!x || !c) {
-    jclass e = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
-    if (e) (*env)->ThrowNew(env, e, "direct ByteBuffers required");
-    return;
-  }
+  if (!direct_sizes_ok(env, n, J, batch)) return;
+  const double* x = (const double*)direct_buffer(env, xbuf, (long long)batch * n, "signal");
+  if (!x) return;
+  double* c = (double*)direct_buffer(env, cbuf, (long long)batch * (J + 1) * n, "coefficient");
+  if (!c) return;
   const int st = jw_modwt_forward((const jw_modwt_plan*)(intptr_t)plan, x, c, (long)n, J, batch,
                                   method, JW_HOST, NULL);
   if (st != JW_OK) jw_throw(env, st);
@@ -197,13 +258,12 @@ JNIEXPORT void JNICALL Java_jwave_hip_HipMODWTTransform_nInverseDirect(
     JNIEnv* env, jclass cls, jlong plan, jobject cbuf, jobject xbuf, jlong n, jint J, jint batch,
     jint method) {
   (void)cls;
-  const double* c = (const double*)(*env)->GetDirectBufferAddress(env, cbuf);
-  double* x = (double*)(*env)->GetDirectBufferAddress(env, xbuf);
-  if (!x || !c) {
-    jclass e = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
-    if (e) (*env)->ThrowNew(env, e, "direct ByteBuffers required");
-    return;
-  }
+  if (!direct_sizes_ok(env, n, J, batch)) return;
+  const double* c =
+      (const double*)direct_buffer(env, cbuf, (long long)batch * (J + 1) * n, "coefficient");
+  if (!c) return;
+  double* x = (double*)direct_buffer(env, xbuf, (long long)batch * n, "signal");
+  if (!x) return;
   const int st = jw_modwt_inverse((const jw_modwt_plan*)(intptr_t)plan, c, x, (long)n, J, batch,
                                   method, JW_HOST, NULL);
   if (st != JW_OK) jw_throw(env, st);
@@ -366,11 +426,12 @@ JNIEXPORT jobjectArray JNICALL Java_jwave_hip_HipContinuousWaveletTransform_nTra
 
 /* ---------------------------------------------------------------- FFT */
 /* FastFourierTransform.forward/reverse(Complex[]) on interleaved (re, im) doubles:
- * dir 0 forward, 1 reverse (with the reference's 1/n). */
+ * dir 0 forward, 1 reverse (with the reference's 1/n); arith JW_ARITH_STRICT runs the
+ * reference's own algorithm (bit-identical for power-of-two lengths). */
 JNIEXPORT jdoubleArray JNICALL Java_jwave_hip_HipFastFourierTransform_nFFT(JNIEnv* env,
                                                                            jclass cls,
                                                                            jdoubleArray reim,
-                                                                           jint dir) {
+                                                                           jint dir, jint arith) {
   (void)cls;
   jsize m = 0;
   double* in = copy_in(env, reim, &m);
@@ -382,8 +443,8 @@ JNIEXPORT jdoubleArray JNICALL Java_jwave_hip_HipFastFourierTransform_nFFT(JNIEn
     return NULL;
   }
   const long n = (long)m / 2;
-  const int st = dir == 0 ? jw_fft_forward(in, out, n, 1, JW_HOST, NULL)
-                          : jw_fft_reverse(in, out, n, 1, JW_HOST, NULL);
+  const int st = dir == 0 ? jw_fft_forward_ex(in, out, n, 1, arith, JW_HOST, NULL)
+                          : jw_fft_reverse_ex(in, out, n, 1, arith, JW_HOST, NULL);
   free(in);
   jdoubleArray res = NULL;
   if (st == JW_OK && (res = (*env)->NewDoubleArray(env, m)) != NULL)

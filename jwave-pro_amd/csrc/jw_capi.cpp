@@ -1,6 +1,7 @@
 // jw_capi.cpp -- the extern "C" boundary (include/jwave_hip.h): argument validation with the
 // reference's exception classes and messages, plan objects, host<->HBM staging.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -33,19 +34,68 @@ int fail(int code, const char* fmt, ...) {
 
 void clear_error() { g_err[0] = '\0'; }
 
-void keep_pool_memory() {
-  static std::mutex mu;
-  static bool done[64] = {};
+// ---- private memory pools (one per device), calls in flight, cache registry ----
+namespace {
+std::mutex g_pool_mu;
+hipMemPool_t g_pools[64] = {};
+std::atomic<uint64_t> g_used_devices{0};  // bit d: a call ran on device d
+}  // namespace
+
+hipMemPool_t device_pool() {
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
-  std::lock_guard<std::mutex> lk(mu);
-  if (done[dev]) return;
-  done[dev] = true;
-  hipMemPool_t pool = nullptr;
-  if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess && pool) {
-    uint64_t keep = UINT64_MAX;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  if (!g_pools[dev]) {
+    hipMemPoolProps props{};
+    props.allocType = hipMemAllocationTypePinned;
+    props.handleTypes = hipMemHandleTypeNone;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = dev;
+    hipMemPool_t pool = nullptr;
+    if (hipMemPoolCreate(&pool, &props) != hipSuccess) return nullptr;
+    uint64_t keep = UINT64_MAX;  // keep freed workspaces for the next call
     (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    g_pools[dev] = pool;
   }
+  return g_pools[dev];
+}
+
+void trim_pools() {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  for (hipMemPool_t p : g_pools)
+    if (p) (void)hipMemPoolTrimTo(p, 0);
+}
+
+std::shared_mutex& api_mutex() {
+  static std::shared_mutex m;
+  return m;
+}
+
+void note_device_used(int dev) {
+  if (dev >= 0 && dev < 64) g_used_devices.fetch_or(1ULL << dev, std::memory_order_relaxed);
+}
+
+namespace {
+std::vector<CacheBase*>& cache_registry() {
+  static std::vector<CacheBase*> r;
+  return r;
+}
+std::mutex& registry_mutex() {
+  static std::mutex m;
+  return m;
+}
+}  // namespace
+
+void register_cache(CacheBase* c) {
+  std::lock_guard<std::mutex> lk(registry_mutex());
+  cache_registry().push_back(c);
+}
+
+size_t release_all_caches() {
+  std::lock_guard<std::mutex> lk(registry_mutex());
+  size_t b = 0;
+  for (CacheBase* c : cache_registry()) b += c->clear();
+  return b;
 }
 
 namespace {
@@ -63,21 +113,17 @@ int floor_log2(long n) {
 
 bool is_binary(long n) { return n > 0 && (n & (n - 1)) == 0; }  // MathToolKit.isBinary :185-188
 
-// JW_HOST staging (what a JNI crossing with double[] uses): per host thread and device, a
-// staging context whose HBM buffers only grow (no hipMalloc / hipFree per call: both
-// synchronise the device and would serialise concurrent Java threads), two pinned bounce
-// buffers that pipeline the pageable-memory copies (memcpy of chunk k+1 beside the DMA of
-// chunk k), and a private non-blocking stream when the caller passes none (threads never
-// meet on the null stream).
+// JW_HOST staging (what a JNI crossing with double[] uses): per host thread and device, two
+// pinned bounce buffers that pipeline the pageable-memory copies (memcpy of chunk k+1 beside
+// the DMA of chunk k) and a private non-blocking stream when the caller passes none (threads
+// never meet on the null stream).  The HBM copies of the caller's arrays come from the
+// library's memory pool per call (stream-ordered: no hipMalloc / hipFree, which synchronise
+// the device and would serialise concurrent Java threads).
 constexpr size_t kPinDoubles = (size_t)4 << 20;  // 32 MiB per bounce buffer
 
 struct HostStage {
   int dev = -1;
   hipStream_t own = nullptr;
-  double* din = nullptr;
-  size_t din_cap = 0;
-  double* dout = nullptr;
-  size_t dout_cap = 0;
   double* pin[2] = {nullptr, nullptr};
   hipEvent_t ev[2] = {nullptr, nullptr};
 
@@ -85,8 +131,6 @@ struct HostStage {
     if (dev < 0) return;
     (void)hipSetDevice(dev);
     if (own) (void)hipStreamSynchronize(own);
-    (void)hipFree(din);
-    (void)hipFree(dout);
     for (int i = 0; i < 2; ++i) {
       if (pin[i]) (void)hipHostFree(pin[i]);
       if (ev[i]) (void)hipEventDestroy(ev[i]);
@@ -102,16 +146,6 @@ struct HostStage {
                                hipHostMallocDefault));
       JW_HIP_TRY(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
     }
-    return JW_OK;
-  }
-
-  static int grow(double** p, size_t* cap, size_t n) {
-    if (n <= *cap) return JW_OK;
-    if (*p) JW_HIP_TRY(hipFree(*p));
-    *p = nullptr;
-    *cap = 0;
-    JW_HIP_TRY(hipMalloc((void**)p, n * sizeof(double)));
-    *cap = n;
     return JW_OK;
   }
 
@@ -177,22 +211,28 @@ int check_where(int where) {
 
 template <class F>
 int run(int where, void* stream, const double* in, size_t nin, double* out, size_t nout, F&& f) {
+  std::shared_lock<std::shared_mutex> in_flight(api_mutex());
+  int dev = 0;
+  JW_HIP_TRY(hipGetDevice(&dev));
+  note_device_used(dev);
   hipStream_t s = (hipStream_t)stream;
   if (where == JW_DEVICE) return f(in, out, s);
   HostStage* hs = nullptr;
   int st = host_stage(&hs);
   if (st != JW_OK) return st;
   if (!s) s = hs->own;
-  if ((st = HostStage::grow(&hs->din, &hs->din_cap, nin)) != JW_OK) return st;
-  if ((st = HostStage::grow(&hs->dout, &hs->dout_cap, nout)) != JW_OK) return st;
-  if ((st = hs->put(hs->din, in, nin, s)) != JW_OK) return st;
-  st = f(hs->din, hs->dout, s);
-  if (st != JW_OK) {
-    (void)hipStreamSynchronize(s);  // the staging buffers are reused by the next call
-    return st;
-  }
-  if ((st = hs->get(out, hs->dout, nout, s)) != JW_OK) return st;
-  JW_HIP_TRY(hipStreamSynchronize(s));
+  double *din = nullptr, *dout = nullptr;
+  {
+    StreamAllocs mem(s);
+    JW_HIP_TRY(mem.alloc(&din, nin * sizeof(double)));
+    JW_HIP_TRY(mem.alloc(&dout, nout * sizeof(double)));
+    if ((st = hs->put(din, in, nin, s)) == JW_OK) st = f(din, dout, s);
+    if (st == JW_OK) st = hs->get(out, dout, nout, s);
+  }  // freed in stream order
+  const hipError_t e = hipStreamSynchronize(s);
+  if (st != JW_OK) return st;
+  if (e != hipSuccess)
+    return fail(JW_ERR_DEVICE, "hipStreamSynchronize failed: %s", hipGetErrorString(e));
   return JW_OK;
 }
 
@@ -222,7 +262,61 @@ extern "C" {
 
 const char* jw_last_error(void) { return g_err; }
 
-const char* jw_version(void) { return "jwave-pro_amd 0.1.0 (gfx950)"; }
+const char* jw_version(void) { return "jwave-pro_amd 0.3.0 (gfx950)"; }
+
+// ---------------------------------------------------------------------------------------- device
+int jw_device_count(int* count) {
+  clear_error();
+  if (!count) return fail(JW_ERR_ILLEGAL_ARGUMENT, "count pointer is null");
+  *count = 0;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return JW_OK;  // no HIP device visible
+  }
+  *count = n;
+  return JW_OK;
+}
+
+int jw_set_device(int ordinal) {
+  clear_error();
+  if (ordinal < 0)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "device ordinal must be >= 0, got %d", ordinal);
+  int n = 0;
+  jw_device_count(&n);
+  if (ordinal >= n)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "device ordinal %d out of range: %d HIP device(s) visible",
+                ordinal, n);
+  JW_HIP_TRY(hipSetDevice(ordinal));
+  return JW_OK;
+}
+
+int jw_get_device(int* ordinal) {
+  clear_error();
+  if (!ordinal) return fail(JW_ERR_ILLEGAL_ARGUMENT, "ordinal pointer is null");
+  JW_HIP_TRY(hipGetDevice(ordinal));
+  return JW_OK;
+}
+
+// Frees every table the library caches (FFT twiddles, chirp-z tables, MODWT filter spectra and
+// pair tables) on every device and returns the memory pools' unused workspace memory.  Calls
+// in flight on other threads finish first (they hold the API lock shared); kernels they queued
+// asynchronously (JW_DEVICE) are waited for before anything is freed.
+long jw_release_caches(void) {
+  clear_error();
+  std::unique_lock<std::shared_mutex> lk(api_mutex());
+  int cur = 0;
+  const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+  const uint64_t used = g_used_devices.load();
+  for (int d = 0; d < 64; ++d) {
+    if (!(used >> d & 1)) continue;
+    if (hipSetDevice(d) == hipSuccess) (void)hipDeviceSynchronize();
+  }
+  if (have_cur) (void)hipSetDevice(cur);
+  const size_t freed = release_all_caches();
+  trim_pools();
+  return (long)freed;
+}
 
 // ---------------------------------------------------------------- MODWT
 int jw_modwt_plan_create(jw_modwt_plan** plan, const double* scaling_dec,
@@ -404,8 +498,10 @@ static int fft_call(int S, int arith, const double* in, double* out, long n, int
   if (n == 0 || batch == 0) return JW_OK;
   if (!in || !out) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
   const size_t elems = (size_t)2 * n * batch;
-  // STRICT: the reference's own FFT (jw_jfft.hip) for power-of-two n <= 2^24
-  const bool strict = arith == JW_ARITH_STRICT && (n & (n - 1)) == 0 && n <= (1L << 24);
+  // STRICT: the reference's own FFT (jw_jfft.hip): radix 2 for powers of two <= 2^24,
+  // Bluestein for other n <= 2^23
+  const bool strict = arith == JW_ARITH_STRICT && ((n & (n - 1)) == 0 ? n <= (1L << 24)
+                                                                      : n <= (1L << 23));
   return run(where, stream, in, elems, out, elems, [&](const double* di, double* dout, hipStream_t s) {
     return strict ? fft_strict_device(S, di, dout, n, batch, s)
                   : fft_device(S, di, dout, n, batch, s);

@@ -10,11 +10,9 @@ namespace jw {
 namespace fft {
 
 namespace {
-std::mutex g_mu;
-// per (device, N): device memory owned for the library's lifetime.  Keyed by the calling
-// thread's current device, so one process driving several GPUs (a JVM with a thread per
-// GPU) never hands one device's tables to another.
-std::map<std::pair<int, long>, Tables> g_tables;
+// per (device, N): the calling thread's current device, so one process driving several GPUs (a
+// JVM with a thread per GPU) never hands one device's tables to another.
+DevCache<std::pair<int, long>> g_tables(1UL << 30);
 
 void fill(cplx* h, long n, long N, long stride) {
   const long double two_pi = 6.283185307179586476925286766559005768L;
@@ -28,29 +26,27 @@ void fill(cplx* h, long n, long N, long stride) {
 int tables(long N, Tables* out) {
   int dev = 0;
   JW_HIP_TRY(hipGetDevice(&dev));
-  const std::pair<int, long> key(dev, N);
-  std::lock_guard<std::mutex> lk(g_mu);
-  auto it = g_tables.find(key);
-  if (it != g_tables.end()) {
-    *out = it->second;
-    return JW_OK;
-  }
   int logN = 0;
   while ((1L << logN) < N) ++logN;
   const int logQ = (logN + 1) / 2;
   const long Q = 1L << logQ, NH = N >> logQ > 0 ? N >> logQ : 1;
   const long total = 512 + Q + NH;
-  cplx* h = new cplx[total];
-  fill(h, 512, 512, 1);
-  fill(h + 512, Q, N, 1);
-  fill(h + 512 + Q, NH, N, Q);
-  cplx* d = nullptr;
-  hipError_t e = hipMalloc((void**)&d, total * sizeof(cplx));
-  if (e == hipSuccess) e = hipMemcpy(d, h, total * sizeof(cplx), hipMemcpyHostToDevice);
-  delete[] h;
-  if (e != hipSuccess) {
-    if (d) (void)hipFree(d);
-    return fail(JW_ERR_DEVICE, "FFT twiddle table for N=%ld: %s", N, hipGetErrorString(e));
+  const std::pair<int, long> key(dev, N);
+  const cplx* d = (const cplx*)g_tables.find(key);
+  if (!d) {  // small (512 + 2 sqrt(N) entries): built with a synchronous copy
+    cplx* h = new cplx[total];
+    fill(h, 512, 512, 1);
+    fill(h + 512, Q, N, 1);
+    fill(h + 512 + Q, NH, N, Q);
+    cplx* p = nullptr;
+    hipError_t e = hipMalloc((void**)&p, total * sizeof(cplx));
+    if (e == hipSuccess) e = hipMemcpy(p, h, total * sizeof(cplx), hipMemcpyHostToDevice);
+    delete[] h;
+    if (e != hipSuccess) {
+      if (p) (void)hipFree(p);
+      return fail(JW_ERR_DEVICE, "FFT twiddle table for N=%ld: %s", N, hipGetErrorString(e));
+    }
+    d = (const cplx*)g_tables.insert(key, p, total * sizeof(cplx));
   }
   Tables t;
   t.N = N;
@@ -58,7 +54,6 @@ int tables(long N, Tables* out) {
   t.w512 = d;
   t.lo = d + 512;
   t.hi = d + 512 + Q;
-  g_tables[key] = t;
   *out = t;
   return JW_OK;
 }

@@ -5,7 +5,11 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <map>
+#include <mutex>
+#include <shared_mutex>
 #include <string>
+#include <utility>
 
 #include "jwave_hip.h"
 
@@ -27,11 +31,13 @@ void clear_error();
                         __FILE__, __LINE__);                                               \
   } while (0)
 
-// The device's default memory pool keeps what the workspaces free instead of returning it to
-// the driver at every synchronisation (the default release threshold is 0): without this a
-// call whose workspace is several GB (the 2-D FWT of cfg4: 6.4 GB) re-maps it every time,
-// ~200 ms per call on some boxes.  Set once per device, on first use.
-void keep_pool_memory();
+// Workspaces come from a private stream-ordered memory pool per device (never the device's
+// default pool, which PyTorch or a JVM's other libraries may tune).  The pool keeps what the
+// workspaces free, so a call whose workspace is several GB (the 2-D FWT of cfg4: 6.4 GB) does
+// not re-map it every time (~200 ms per call on some boxes when released at every sync); an
+// allocation that fails trims the pool and retries once; jw_release_caches() trims it.
+hipMemPool_t device_pool();  // the calling thread's current device's pool (created lazily)
+void trim_pools();
 
 // Stream-ordered device allocations of one call, released on every exit path (the early
 // returns of JW_HIP_TRY included): hipFreeAsync on the call's stream, so the memory is
@@ -48,9 +54,16 @@ class StreamAllocs {
   hipError_t alloc(T** out, size_t bytes) {
     *out = nullptr;
     if (n_ == kMax) return hipErrorOutOfMemory;
-    keep_pool_memory();
+    hipMemPool_t pool = device_pool();
+    if (!pool) return hipErrorOutOfMemory;
     void* p = nullptr;
-    const hipError_t e = hipMallocAsync(&p, bytes, s_);
+    hipError_t e = hipMallocFromPoolAsync(&p, bytes, pool, s_);
+    if (e == hipErrorOutOfMemory) {  // give back what the pool holds unused, then retry once
+      (void)hipGetLastError();
+      (void)hipStreamSynchronize(s_);
+      (void)hipMemPoolTrimTo(pool, 0);
+      e = hipMallocFromPoolAsync(&p, bytes, pool, s_);
+    }
     if (e == hipSuccess) {
       p_[n_++] = p;
       *out = (T*)p;
@@ -65,10 +78,97 @@ class StreamAllocs {
   int n_ = 0;
 };
 
+// Calls in flight hold this shared; jw_release_caches() takes it exclusively, so no call is
+// between looking up a cached table and launching the kernels that read it while it frees.
+std::shared_mutex& api_mutex();
+void note_device_used(int dev);
+
+// ---- library-owned device tables (twiddles, chirp-z, filter spectra, pair tables) ----
+// Built on the caller's stream, synchronised once, then published; no lock is held across
+// device work.  Each cache keeps at most `budget` bytes; beyond that a call builds a table of
+// its own (stream-ordered, freed after the call).  jw_release_caches() clears them all.
+class CacheBase {
+ public:
+  virtual ~CacheBase() = default;
+  virtual size_t clear() = 0;
+};
+void register_cache(CacheBase* c);
+size_t release_all_caches();  // bytes freed; the caller holds api_mutex() exclusively
+
+template <class Key>
+class DevCache : public CacheBase {
+ public:
+  explicit DevCache(size_t budget) : budget_(budget) { register_cache(this); }
+  const void* find(const Key& k) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = m_.find(k);
+    return it == m_.end() ? nullptr : it->second.first;
+  }
+  bool fits(size_t bytes) {
+    std::lock_guard<std::mutex> lk(mu_);
+    return bytes_ + bytes <= budget_;
+  }
+  // takes ownership of p (hipMalloc'd, complete); returns the entry to use -- another
+  // thread's if it raced us, in which case p is freed
+  const void* insert(const Key& k, void* p, size_t bytes) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = m_.find(k);
+    if (it != m_.end()) {
+      (void)hipFree(p);
+      return it->second.first;
+    }
+    m_.emplace(k, std::make_pair(p, bytes));
+    bytes_ += bytes;
+    return p;
+  }
+  size_t clear() override {
+    std::lock_guard<std::mutex> lk(mu_);
+    const size_t b = bytes_;
+    for (auto& e : m_) (void)hipFree(e.second.first);
+    m_.clear();
+    bytes_ = 0;
+    return b;
+  }
+
+ private:
+  std::mutex mu_;
+  std::map<Key, std::pair<void*, size_t>> m_;
+  size_t bytes_ = 0;
+  size_t budget_;
+};
+
+// A cached table of `bytes` filled by fill(void* dst) on stream s (JW_OK or an error), or a
+// per-call one past the budget.
+template <class Key, class Fill>
+int cached_table(DevCache<Key>& cache, const Key& key, size_t bytes, StreamAllocs& mem,
+                 hipStream_t s, const void** out, Fill&& fill) {
+  if ((*out = cache.find(key)) != nullptr) return JW_OK;
+  if (!cache.fits(bytes)) {
+    void* p = nullptr;
+    JW_HIP_TRY(mem.alloc(&p, bytes));
+    *out = p;
+    return fill(p);
+  }
+  void* p = nullptr;
+  JW_HIP_TRY(hipMalloc(&p, bytes));
+  const int st = fill(p);
+  const hipError_t e = hipStreamSynchronize(s);  // complete before another thread may read it
+  if (st != JW_OK || e != hipSuccess) {
+    (void)hipFree(p);
+    return st != JW_OK ? st : fail(JW_ERR_DEVICE, "table build: %s", hipGetErrorString(e));
+  }
+  *out = cache.insert(key, p, bytes);
+  return JW_OK;
+}
+
 // Host -> device copy that stays asynchronous: the bytes are copied into a heap buffer that
 // a host callback on the stream frees once the transfer has been reached (the caller's
 // buffer may go away as soon as this returns).
 hipError_t upload_async(void* dst, const void* src, size_t bytes, hipStream_t s);
+
+// Correctly rounded sin and cos of x (jw_crmath.cc): the values of Math.sin / Math.cos the
+// STRICT FFT tables use.
+void cr_sincos(double x, double* s, double* c);
 
 // Filter taps passed to kernels by value (lands in SGPRs: wave-uniform).
 struct Taps {
@@ -112,9 +212,6 @@ int modwt_forward_strict_device(const ModwtPlan& p, const double* x, double* coe
 int modwt_inverse_strict_device(const ModwtPlan& p, const double* coeffs, double* x, long n,
                                 int J, int batch, const bool* fft_level, hipStream_t s);
 int fft_strict_device(int S, const double* in, double* out, long n, long batch, hipStream_t s);
-// Frees the cached twiddle / filter-spectrum / chirp tables of every FFT path (bytes freed).
-size_t release_strict_caches();
-size_t release_fft_caches();
 // One direct MODWT level (circularConvolve{,Adjoint}, :677-716) on batch rows with strides:
 // forward W_j, V_j <- V_{j-1}; inverse out = g_j^T V_j + h_j^T W_j.
 int modwt_level_forward_device(const ModwtPlan& p, int j, const double* v, long vs, double* w,

@@ -12,82 +12,11 @@
 #include <type_traits>
 #include <vector>
 
-#include "jw_jfft.hpp"
+#include "jw_jfft_host.hpp"
 
 namespace jw {
 namespace jf {
 namespace {
-
-constexpr long kLineMax = 4096;  // whole transform in one column up to here
-
-// ---------------------------------------------------------------------------------------
-// Device caches: built on the caller's stream, synchronised once, then published.  No lock is
-// held across device work.  At most kCacheBytes per cache: past that a call builds its own
-// table (stream-ordered, freed after the call).  jw_release_caches() frees them.
-// ---------------------------------------------------------------------------------------
-constexpr size_t kCacheBytes = 2UL << 30;
-
-template <class Key>
-class DevCache {
- public:
-  const void* find(const Key& k) {
-    std::lock_guard<std::mutex> lk(mu_);
-    auto it = m_.find(k);
-    return it == m_.end() ? nullptr : it->second.first;
-  }
-  bool fits(size_t bytes) {
-    std::lock_guard<std::mutex> lk(mu_);
-    return bytes_ + bytes <= kCacheBytes;
-  }
-  // takes ownership of p (complete); returns the entry to use -- another thread's if it
-  // raced us, in which case p is freed
-  const void* insert(const Key& k, void* p, size_t bytes) {
-    std::lock_guard<std::mutex> lk(mu_);
-    auto it = m_.find(k);
-    if (it != m_.end()) {
-      (void)hipFree(p);
-      return it->second.first;
-    }
-    m_.emplace(k, std::make_pair(p, bytes));
-    bytes_ += bytes;
-    return p;
-  }
-  size_t clear() {
-    std::lock_guard<std::mutex> lk(mu_);
-    const size_t b = bytes_;
-    for (auto& e : m_) (void)hipFree(e.second.first);
-    m_.clear();
-    bytes_ = 0;
-    return b;
-  }
-
- private:
-  std::mutex mu_;
-  std::map<Key, std::pair<void*, size_t>> m_;
-  size_t bytes_ = 0;
-};
-
-template <class Key, class Fill>
-int cached_table(DevCache<Key>& cache, const Key& key, size_t bytes, StreamAllocs& mem,
-                 hipStream_t s, const void** out, Fill&& fill) {
-  if ((*out = cache.find(key)) != nullptr) return JW_OK;
-  if (!cache.fits(bytes)) {
-    void* p = nullptr;
-    JW_HIP_TRY(mem.alloc(&p, bytes));
-    *out = p;
-    return fill(p);
-  }
-  void* p = nullptr;
-  JW_HIP_TRY(hipMalloc(&p, bytes));
-  int st = fill(p);
-  const hipError_t e = hipStreamSynchronize(s);  // complete before other threads may see it
-  if (st != JW_OK || e != hipSuccess) {
-    (void)hipFree(p);
-    return st != JW_OK ? st : fail(JW_ERR_DEVICE, "table build: %s", hipGetErrorString(e));
-  }
-  *out = cache.insert(key, p, bytes);
-  return JW_OK;
-}
 
 // ---------------------------------------------------------------------------------------
 // Twiddles: Tw[half + k] = wn_k of the stage of size 2 half, by the reference's recurrence
@@ -96,7 +25,7 @@ int cached_table(DevCache<Key>& cache, const Key& key, size_t bytes, StreamAlloc
 // transposed, Tw2[l lc2 + m] = Tw[m lc1 + l] (l < lc1, m < lc2 = n / lc1).
 // ---------------------------------------------------------------------------------------
 using TwKey = std::tuple<int, long, int, int>;  // device, n, inverse, lc1
-DevCache<TwKey> g_tw;
+DevCache<TwKey> g_tw(kCacheBytes);
 
 constexpr double kJavaPi = 3.141592653589793;  // Math.PI
 
@@ -105,7 +34,8 @@ void java_twiddles(long n, bool inverse, std::vector<cplx>& tw) {
   for (long half = 1; half < n; half <<= 1) {
     const long size = 2 * half;
     const double angle = 2 * kJavaPi / (double)size * (double)(inverse ? 1 : -1);
-    const double wr = std::cos(angle), wi = std::sin(angle);
+    double wr, wi;  // Math.cos(angle), Math.sin(angle), correctly rounded (jw_crmath.cc)
+    cr_sincos(angle, &wi, &wr);
     double nr = 1.0, ni = 0.0;  // wn = new Complex(1, 0)
     for (long k = 0; k < half; ++k) {
       tw[half + k] = make_double2(nr, ni);
@@ -116,15 +46,7 @@ void java_twiddles(long n, bool inverse, std::vector<cplx>& tw) {
   }
 }
 
-struct Tw {
-  long n = 0;
-  int lc1 = 0;
-  const cplx* p1 = nullptr;
-  const cplx* p2 = nullptr;
-};
-
-// pass-1 length of an n-point transform (n itself when it runs in one column)
-int split_lc1(long n) { return n <= kLineMax ? (int)n : 1 << (ilog2(n) / 2); }
+}  // namespace
 
 int twiddles(long n, bool inverse, int lc1, Tw* out, StreamAllocs& mem, hipStream_t s) {
   int dev = 0;
@@ -155,195 +77,14 @@ int twiddles(long n, bool inverse, int lc1, Tw* out, StreamAllocs& mem, hipStrea
   return JW_OK;
 }
 
-// ---------------------------------------------------------------------------------------
-// Launch helpers: runtime column length -> template instantiation
-// ---------------------------------------------------------------------------------------
-#define JF_CASE(V) \
-  case V:          \
-    return f(std::integral_constant<int, V>{});
-
-template <class F>
-int with_lc(long lc, F&& f) {
-  switch (lc) {
-    JF_CASE(2) JF_CASE(4) JF_CASE(8) JF_CASE(16) JF_CASE(32) JF_CASE(64) JF_CASE(128)
-    JF_CASE(256) JF_CASE(512) JF_CASE(1024) JF_CASE(2048) JF_CASE(4096)
-    default:
-      return fail(JW_ERR_UNSUPPORTED, "Java-order FFT: line length %ld unsupported", lc);
-  }
-}
-template <class F>
-int with_big_lc(long lc, F&& f) {
-  switch (lc) {
-    JF_CASE(64) JF_CASE(128) JF_CASE(256) JF_CASE(512) JF_CASE(1024) JF_CASE(2048) JF_CASE(4096)
-    default:
-      return fail(JW_ERR_UNSUPPORTED, "Java-order FFT: column length %ld unsupported", lc);
-  }
-}
-#undef JF_CASE
-
-template <int LC, class K, class... A>
-int launch_grid(K kern, long blocks, hipStream_t s, A... args) {
-  const size_t lds = Geo<LC>::LDS_BYTES;
-  JW_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)lds));
-  if (blocks <= 0) return JW_OK;
-  if (blocks >= (1L << 24))
-    return fail(JW_ERR_UNSUPPORTED, "Java-order FFT: grid of %ld workgroups", blocks);
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kNT), lds, s, args...);
-  JW_HIP_TRY(hipGetLastError());
-  return JW_OK;
-}
-
-// ---------------------------------------------------------------------------------------
-// Functors (natural indices; see jw_jfft.hpp)
-// ---------------------------------------------------------------------------------------
-struct RowsR {  // real rows -> Complex(x, 0) (:766-769)
-  const double* p;
-  long st;
-  __device__ cplx operator()(long it, long i) const { return make_double2(p[it * st + i], 0.0); }
-};
-struct RowsC {
-  const cplx* p;
-  long st;
-  __device__ cplx operator()(long it, long i) const { return p[it * st + i]; }
-};
-struct OutC {
-  cplx* p;
-  long st;
-  __device__ void operator()(long it, long i, cplx v) const { p[it * st + i] = v; }
-};
-struct OutCS {  // x[i].mul(1.0 / n) for a reverse transform (FastFourierTransform.java:207-211)
-  cplx* p;
-  long st;
-  double sc;
-  int do_scale;
-  __device__ void operator()(long it, long i, cplx v) const {
-    p[it * st + i] = do_scale ? jscale(v, sc) : v;
-  }
-};
-struct OutR {
-  double* p;
-  long st;
-  __device__ void operator()(long it, long i, double v) const { p[it * st + i] = v; }
-};
-// NF row outputs, stream f at p + f * fst
-struct OutF {
-  cplx* p;
-  long st, fst;
-  __device__ void operator()(int f, long it, long j, cplx v) const { p[f * fst + it * st + j] = v; }
-};
-// NIN column inputs, stream s at p + s * sst
-struct InS {
-  const cplx* p;
-  long st, sst;
-  __device__ cplx operator()(int s, long it, long i) const { return p[s * sst + it * st + i]; }
-};
-struct PowPost {  // result[i].mul(1.0 / n).getReal() (:207-211, :781-783)
-  double inv_n;
-  __device__ double operator()(int, long, long, cplx v) const { return v.x * inv_n; }
-};
-// forward level: signalFFT[i].mul(filterFFT[i]), f = 0 -> h_j (W_j), f = 1 -> g_j (V_j) (:775-778)
-struct FwdMid {
-  const cplx* fh;
-  const cplx* fg;
-  __device__ cplx operator()(int f, long, long i, cplx x) const { return jmul(x, (f ? fg : fh)[i]); }
-};
-// adjoint: signalFFT[i].mul(filterFFT[i].conjugate()) (:820-824); items [0, nb) are V_j (g_j),
-// [nb, 2 nb) are W_j (h_j)
-struct AdjMid {
-  const cplx* fg;
-  const cplx* fh;
-  long nb;
-  __device__ cplx operator()(int, long it, long i, cplx x) const {
-    const cplx f = (it < nb ? fg : fh)[i];
-    return jmul(x, make_double2(f.x, -f.y));
-  }
-};
-// line kernels (n <= kLineMax)
-struct LineIn {
-  const double* p0;
-  long st0;
-  const double* p1;
-  long st1;
-  __device__ double operator()(int s, long ln, int r) const {
-    return s == 0 ? p0[ln * st0 + r] : p1[ln * st1 + r];
-  }
-};
-struct LineOut {
-  double* p0;
-  long st0;
-  double* p1;
-  long st1;
-  __device__ void operator()(int f, long ln, int r, double v) const {
-    if (f == 0) {
-      p0[ln * st0 + r] = v;
-    } else {
-      p1[ln * st1 + r] = v;
-    }
-  }
-};
-struct LineFwdMid {
-  const cplx* fh;
-  const cplx* fg;
-  __device__ cplx operator()(int, int f, long i, cplx x) const { return jmul(x, (f ? fg : fh)[i]); }
-};
-struct LineAdjMid {  // s = 0: V_j with g_j, s = 1: W_j with h_j
-  const cplx* fg;
-  const cplx* fh;
-  __device__ cplx operator()(int s, int, long i, cplx x) const {
-    const cplx f = (s ? fh : fg)[i];
-    return jmul(x, make_double2(f.x, -f.y));
-  }
-};
-
-// ---------------------------------------------------------------------------------------
-// Natural-order transforms of `items` rows: in (RowsR / RowsC) -> out (OutCS)
-// ---------------------------------------------------------------------------------------
-template <class In>
-int fft_rows(long n, bool inverse, long items, In in, OutCS out, StreamAllocs& mem,
-             hipStream_t s) {
-  const int lc1 = split_lc1(n);
-  Tw tw;
-  int st = twiddles(n, inverse, lc1, &tw, mem, s);
-  if (st != JW_OK) return st;
-  if (n <= kLineMax) {
-    return with_lc(n, [&](auto LCc) -> int {
-      constexpr int LC = decltype(LCc)::value;
-      return launch_grid<LC>(kline_fft<LC, In, OutCS>, (items + Geo<LC>::T - 1) / Geo<LC>::T, s,
-                             in, out, items, tw.p1, 1.0, 0);
-    });
-  }
-  const long lc2 = n / lc1;
-  const long chunk = std::max(1L, std::min<long>(items, (1L << 30) / (n * (long)sizeof(cplx))));
-  cplx* Z = nullptr;
-  JW_HIP_TRY(mem.alloc(&Z, (size_t)chunk * n * sizeof(cplx)));
-  for (long i0 = 0; i0 < items && st == JW_OK; i0 += chunk) {
-    const long ni = std::min(chunk, items - i0);
-    In in_c = in;
-    in_c.p += i0 * in.st;
-    OutCS out_c = out;
-    out_c.p += i0 * out.st;
-    st = with_big_lc(lc1, [&](auto LCc) -> int {
-      constexpr int LC = decltype(LCc)::value;
-      return launch_grid<LC>(kp1<LC, In, OutC>, (lc2 / Geo<LC>::T) * ni, s, in_c, OutC{Z, n},
-                             ilog2(lc2), ni, tw.p1);
-    });
-    if (st != JW_OK) break;
-    st = with_big_lc(lc2, [&](auto LCc) -> int {
-      constexpr int LC = decltype(LCc)::value;
-      return launch_grid<LC>(kp2s<LC, RowsC, OutCS>, (lc1 / Geo<LC>::T) * ni, s, RowsC{Z, n},
-                             out_c, ilog2(lc1), ni, tw.p2);
-    });
-  }
-  return st;
-}
+namespace {
 
 // ---------------------------------------------------------------------------------------
 // MODWT filter spectra: FFT(wrapFilterToSignalLength(upsample(f, j), N)) (:729-741, :770-771),
 // rows [j - 1][0 = h (wavelet), 1 = g (scaling)], natural order; cached per (device, taps, N, J).
 // ---------------------------------------------------------------------------------------
 using SpecKey = std::tuple<int, long, int, std::vector<double>>;
-DevCache<SpecKey> g_spec;
+DevCache<SpecKey> g_spec(kCacheBytes);
 
 // the up-sampled filter of level j (upsample :618-630) wrapped in the reference's order,
 // zero taps included: wrappedFilter[i % N] += filter[i], i ascending
@@ -372,6 +113,7 @@ int filter_spectra(const ModwtPlan& p, long N, int J, const cplx** F, StreamAllo
         double* drows = nullptr;
         JW_HIP_TRY(mem.alloc(&drows, rows.size() * sizeof(double)));
         JW_HIP_TRY(upload_async(drows, rows.data(), rows.size() * sizeof(double), s));
+        if (N & (N - 1)) return bs_spectra_real(N, 2L * J, drows, (cplx*)d, mem, s);
         return fft_rows(N, false, 2L * J, RowsR{drows, N}, OutCS{(cplx*)d, N, 1.0, 0}, mem, s);
       });
   *F = (const cplx*)out;
@@ -580,6 +322,7 @@ int modwt_strict(bool inverse, const ModwtPlan& p, const double* in, double* out
   const cplx* F = nullptr;
   int st = filter_spectra(p, N, J, &F, mem, s);
   if (st != JW_OK) return st;
+  if (N & (N - 1)) return modwt_strict_bs(inverse, p, in, out, N, J, batch, fft, F, mem, s);
   const long rs = (long)(J + 1) * N;
   if (N <= kLineMax) {
     Tw twf, twi;
@@ -628,9 +371,9 @@ int modwt_strict(bool inverse, const ModwtPlan& p, const double* in, double* out
 // ---------------------------------------------------------------------------------------
 // entry points (jw_internal.hpp)
 // ---------------------------------------------------------------------------------------
-bool modwt_strict_fft_supported(long n) {
-  return n >= 2 && (n & (n - 1)) == 0 && n <= (1L << 23);
-}
+// every length the reference's FFT path takes here: powers of two (radix 2) and, through
+// Bluestein with m <= 2^24, any other n <= 2^23
+bool modwt_strict_fft_supported(long n) { return n >= 2 && n <= (1L << 23); }
 
 int modwt_forward_strict_device(const ModwtPlan& p, const double* x, double* coeffs, long n,
                                 int J, int batch, const bool* fft_level, hipStream_t s) {
@@ -650,8 +393,11 @@ int fft_strict_device(int S, const double* in, double* out, long n, long batch, 
                                 hipMemcpyDeviceToDevice, s));
     return JW_OK;
   }
-  if ((n & (n - 1)) != 0 || n > (1L << 24))
-    return fail(JW_ERR_UNSUPPORTED, "Java-order FFT: length %ld", n);
+  if ((n & (n - 1)) != 0) {
+    if (n > (1L << 23)) return fail(JW_ERR_UNSUPPORTED, "Java-order FFT: length %ld > 2^23", n);
+    return jf::bs_fft_strict(S > 0, (const jf::cplx*)in, (jf::cplx*)out, n, batch, s);
+  }
+  if (n > (1L << 24)) return fail(JW_ERR_UNSUPPORTED, "Java-order FFT: length %ld > 2^24", n);
   // in == out is safe: a line is read whole before it is written, and the column path reads
   // the input in pass 1 and writes the output in pass 2 (from the workspace Z)
   StreamAllocs mem(s);
@@ -660,7 +406,5 @@ int fft_strict_device(int S, const double* in, double* out, long n, long batch, 
   return jf::fft_rows(n, S > 0, batch, jf::RowsC{xi, n},
                       jf::OutCS{xo, n, 1.0 / (double)n, S > 0 ? 1 : 0}, mem, s);
 }
-
-size_t release_strict_caches() { return jf::g_tw.clear() + jf::g_spec.clear(); }
 
 }  // namespace jw

@@ -440,3 +440,49 @@ __global__ __launch_bounds__(kNT) void kline_modwt(In in, Mid mid, Out out, long
 
 }  // namespace jf
 }  // namespace jw
+
+namespace jw {
+namespace jf {
+
+// The convolution inside fftBluestein (FastFourierTransform.java:259-324) on whole lines
+// (m = LC <= 4096): a (In, already chirped, zero past n) is FFT'd, multiplied by B = FFT(b)
+// (a[i].mul(b[i]), :300-302), inverse FFT'd without the 1/m, and every point handed to Out
+// (operator()(long line, int r, cplx v)), which applies the reference's post-processing.
+template <int LC, class In, class Out>
+__global__ __launch_bounds__(kNT) void kline_conv(In in, Out out, long nlines,
+                                                  const cplx* __restrict__ B,
+                                                  const cplx* __restrict__ twf,
+                                                  const cplx* __restrict__ twi) {
+  using G = Geo<LC>;
+  extern __shared__ cplx lds[];
+  const int cc = threadIdx.x / G::TPC, tl = threadIdx.x % G::TPC;
+  const long line = (long)blockIdx.x * G::T + cc;
+  const bool valid = line < nlines;
+  cplx* col = lds + cc * G::CS;
+  line_load_rev<LC>(col, tl, [&](long ln, int r) { return valid ? in(ln, r) : cplx{0.0, 0.0}; },
+                    line);
+  col_sync<LC>();
+  run_stages<LC>(col, tl, twf);
+  col_sync<LC>();
+  cplx X[G::EPT];
+#pragma unroll
+  for (int k = 0; k < G::EPT; ++k) X[k] = col[pidx(own_pos<LC>(tl, k))];
+  col_sync<LC>();
+#pragma unroll
+  for (int k = 0; k < G::EPT; ++k) {
+    const int p = own_pos<LC>(tl, k);
+    col[pidx(brev(p, G::LOG))] = jmul(X[k], B[p]);
+  }
+  col_sync<LC>();
+  run_stages<LC>(col, tl, twi);
+  col_sync<LC>();
+  if (!valid) return;
+#pragma unroll
+  for (int k = 0; k < G::EPT; ++k) {
+    const int p = own_pos<LC>(tl, k);
+    out(line, p, col[pidx(p)]);
+  }
+}
+
+}  // namespace jf
+}  // namespace jw

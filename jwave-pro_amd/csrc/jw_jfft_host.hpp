@@ -1,0 +1,222 @@
+// jw_jfft_host.hpp -- host-side helpers of the JW_ARITH_STRICT FFT paths (jw_jfft.hip,
+// jw_jfft_bs.hip): twiddle tables, launch helpers, functors, natural-order transforms of rows.
+#pragma once
+#include <algorithm>
+#include <type_traits>
+
+#include "jw_jfft.hpp"
+
+namespace jw {
+namespace jf {
+
+constexpr long kLineMax = 4096;  // whole transform in one column up to here
+
+constexpr size_t kCacheBytes = 2UL << 30;  // per table cache
+
+struct Tw {
+  long n = 0;
+  int lc1 = 0;
+  const cplx* p1 = nullptr;
+  const cplx* p2 = nullptr;
+};
+
+// pass-1 length of an n-point transform (n itself when it runs in one column)
+inline int split_lc1(long n) { return n <= kLineMax ? (int)n : 1 << (ilog2(n) / 2); }
+
+// Twiddles of an n-point transform in the reference's recurrence order, laid out for a split
+// with pass-1 length lc1 (jw_jfft.hip); cached per (device, n, direction, lc1).
+int twiddles(long n, bool inverse, int lc1, Tw* out, StreamAllocs& mem, hipStream_t s);
+
+// ---------------------------------------------------------------------------------------
+// Launch helpers: runtime column length -> template instantiation
+// ---------------------------------------------------------------------------------------
+#define JF_CASE(V) \
+  case V:          \
+    return f(std::integral_constant<int, V>{});
+
+template <class F>
+inline int with_lc(long lc, F&& f) {
+  switch (lc) {
+    JF_CASE(2) JF_CASE(4) JF_CASE(8) JF_CASE(16) JF_CASE(32) JF_CASE(64) JF_CASE(128)
+    JF_CASE(256) JF_CASE(512) JF_CASE(1024) JF_CASE(2048) JF_CASE(4096)
+    default:
+      return fail(JW_ERR_UNSUPPORTED, "Java-order FFT: line length %ld unsupported", lc);
+  }
+}
+template <class F>
+inline int with_big_lc(long lc, F&& f) {
+  switch (lc) {
+    JF_CASE(64) JF_CASE(128) JF_CASE(256) JF_CASE(512) JF_CASE(1024) JF_CASE(2048) JF_CASE(4096)
+    default:
+      return fail(JW_ERR_UNSUPPORTED, "Java-order FFT: column length %ld unsupported", lc);
+  }
+}
+#undef JF_CASE
+
+template <int LC, class K, class... A>
+int launch_grid(K kern, long blocks, hipStream_t s, A... args) {
+  const size_t lds = Geo<LC>::LDS_BYTES;
+  JW_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)lds));
+  if (blocks <= 0) return JW_OK;
+  if (blocks >= (1L << 24))
+    return fail(JW_ERR_UNSUPPORTED, "Java-order FFT: grid of %ld workgroups", blocks);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kNT), lds, s, args...);
+  JW_HIP_TRY(hipGetLastError());
+  return JW_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// Functors (natural indices; see jw_jfft.hpp)
+// ---------------------------------------------------------------------------------------
+struct RowsR {  // real rows -> Complex(x, 0) (:766-769)
+  const double* p;
+  long st;
+  __device__ cplx operator()(long it, long i) const { return make_double2(p[it * st + i], 0.0); }
+};
+struct RowsC {
+  const cplx* p;
+  long st;
+  __device__ cplx operator()(long it, long i) const { return p[it * st + i]; }
+};
+struct OutC {
+  cplx* p;
+  long st;
+  __device__ void operator()(long it, long i, cplx v) const { p[it * st + i] = v; }
+};
+struct OutCS {  // x[i].mul(1.0 / n) for a reverse transform (FastFourierTransform.java:207-211)
+  cplx* p;
+  long st;
+  double sc;
+  int do_scale;
+  __device__ void operator()(long it, long i, cplx v) const {
+    p[it * st + i] = do_scale ? jscale(v, sc) : v;
+  }
+};
+struct OutR {
+  double* p;
+  long st;
+  __device__ void operator()(long it, long i, double v) const { p[it * st + i] = v; }
+};
+// NF row outputs, stream f at p + f * fst
+struct OutF {
+  cplx* p;
+  long st, fst;
+  __device__ void operator()(int f, long it, long j, cplx v) const { p[f * fst + it * st + j] = v; }
+};
+// NIN column inputs, stream s at p + s * sst
+struct InS {
+  const cplx* p;
+  long st, sst;
+  __device__ cplx operator()(int s, long it, long i) const { return p[s * sst + it * st + i]; }
+};
+struct PowPost {  // result[i].mul(1.0 / n).getReal() (:207-211, :781-783)
+  double inv_n;
+  __device__ double operator()(int, long, long, cplx v) const { return v.x * inv_n; }
+};
+// forward level: signalFFT[i].mul(filterFFT[i]), f = 0 -> h_j (W_j), f = 1 -> g_j (V_j) (:775-778)
+struct FwdMid {
+  const cplx* fh;
+  const cplx* fg;
+  __device__ cplx operator()(int f, long, long i, cplx x) const { return jmul(x, (f ? fg : fh)[i]); }
+};
+// adjoint: signalFFT[i].mul(filterFFT[i].conjugate()) (:820-824); items [0, nb) are V_j (g_j),
+// [nb, 2 nb) are W_j (h_j)
+struct AdjMid {
+  const cplx* fg;
+  const cplx* fh;
+  long nb;
+  __device__ cplx operator()(int, long it, long i, cplx x) const {
+    const cplx f = (it < nb ? fg : fh)[i];
+    return jmul(x, make_double2(f.x, -f.y));
+  }
+};
+// line kernels (n <= kLineMax)
+struct LineIn {
+  const double* p0;
+  long st0;
+  const double* p1;
+  long st1;
+  __device__ double operator()(int s, long ln, int r) const {
+    return s == 0 ? p0[ln * st0 + r] : p1[ln * st1 + r];
+  }
+};
+struct LineOut {
+  double* p0;
+  long st0;
+  double* p1;
+  long st1;
+  __device__ void operator()(int f, long ln, int r, double v) const {
+    if (f == 0) {
+      p0[ln * st0 + r] = v;
+    } else {
+      p1[ln * st1 + r] = v;
+    }
+  }
+};
+struct LineFwdMid {
+  const cplx* fh;
+  const cplx* fg;
+  __device__ cplx operator()(int, int f, long i, cplx x) const { return jmul(x, (f ? fg : fh)[i]); }
+};
+struct LineAdjMid {  // s = 0: V_j with g_j, s = 1: W_j with h_j
+  const cplx* fg;
+  const cplx* fh;
+  __device__ cplx operator()(int s, int, long i, cplx x) const {
+    const cplx f = (s ? fh : fg)[i];
+    return jmul(x, make_double2(f.x, -f.y));
+  }
+};
+
+// ---------------------------------------------------------------------------------------
+// Natural-order transforms of `items` rows: in (RowsR / RowsC) -> out (OutCS)
+// ---------------------------------------------------------------------------------------
+template <class In>
+inline int fft_rows(long n, bool inverse, long items, In in, OutCS out, StreamAllocs& mem,
+             hipStream_t s) {
+  const int lc1 = split_lc1(n);
+  Tw tw;
+  int st = twiddles(n, inverse, lc1, &tw, mem, s);
+  if (st != JW_OK) return st;
+  if (n <= kLineMax) {
+    return with_lc(n, [&](auto LCc) -> int {
+      constexpr int LC = decltype(LCc)::value;
+      return launch_grid<LC>(kline_fft<LC, In, OutCS>, (items + Geo<LC>::T - 1) / Geo<LC>::T, s,
+                             in, out, items, tw.p1, 1.0, 0);
+    });
+  }
+  const long lc2 = n / lc1;
+  const long chunk = std::max(1L, std::min<long>(items, (1L << 30) / (n * (long)sizeof(cplx))));
+  cplx* Z = nullptr;
+  JW_HIP_TRY(mem.alloc(&Z, (size_t)chunk * n * sizeof(cplx)));
+  for (long i0 = 0; i0 < items && st == JW_OK; i0 += chunk) {
+    const long ni = std::min(chunk, items - i0);
+    In in_c = in;
+    in_c.p += i0 * in.st;
+    OutCS out_c = out;
+    out_c.p += i0 * out.st;
+    st = with_big_lc(lc1, [&](auto LCc) -> int {
+      constexpr int LC = decltype(LCc)::value;
+      return launch_grid<LC>(kp1<LC, In, OutC>, (lc2 / Geo<LC>::T) * ni, s, in_c, OutC{Z, n},
+                             ilog2(lc2), ni, tw.p1);
+    });
+    if (st != JW_OK) break;
+    st = with_big_lc(lc2, [&](auto LCc) -> int {
+      constexpr int LC = decltype(LCc)::value;
+      return launch_grid<LC>(kp2s<LC, RowsC, OutCS>, (lc1 / Geo<LC>::T) * ni, s, RowsC{Z, n},
+                             out_c, ilog2(lc1), ni, tw.p2);
+    });
+  }
+  return st;
+}
+
+// Lengths that are not powers of two (jw_jfft_bs.hip): the reference's Bluestein transform.
+int bs_spectra_real(long n, long items, const double* rows, cplx* out, StreamAllocs& mem,
+                    hipStream_t s);
+int bs_fft_strict(bool inverse, const cplx* in, cplx* out, long n, long batch, hipStream_t s);
+int modwt_strict_bs(bool inverse, const ModwtPlan& p, const double* in, double* out, long N,
+                    int J, int batch, const bool* fft, const cplx* F, StreamAllocs& mem,
+                    hipStream_t s);
+
+}  // namespace jf
+}  // namespace jw

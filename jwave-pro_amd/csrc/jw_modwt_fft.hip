@@ -240,55 +240,39 @@ __global__ void chirp_b(cplx* b, const cplx* w, long N, long M) {
 }
 
 // The chirp tables and FFT_M(b) depend on N alone: built once per (device, N) on the device
-// (the first call for a length synchronises its stream once) and kept for the library's
-// lifetime, like the twiddle tables.
-std::mutex g_bs_mu;
-std::map<std::pair<int, long>, Bluestein> g_bs;
+// (the first call for a length synchronises its stream once) and kept, within a 2 GiB budget
+// (past it a call builds its own), until jw_release_caches().  One buffer per key:
+// [c_n, n < N | FFT_M(b) for S = -1 | for S = +1].
+DevCache<std::pair<int, long>> g_bs(2UL << 30);
 
 int bluestein_init(Bluestein* B, long N, long max_items, StreamAllocs& mem, hipStream_t s) {
   int dev = 0;
   JW_HIP_TRY(hipGetDevice(&dev));
-  {
-    std::lock_guard<std::mutex> lk(g_bs_mu);
-    auto it = g_bs.find({dev, N});
-    if (it == g_bs.end()) {
-      Bluestein c;
-      c.N = N;
-      c.M = 1;
-      while (c.M < 2 * N - 1) c.M <<= 1;
-      const long M = c.M;
-      int st = fft::tables(M, &c.T);
-      if (st != JW_OK) return st;
-      cplx *w = nullptr, *bh = nullptr, *tmp = nullptr;
-      hipError_t e = hipMalloc((void**)&w, N * sizeof(cplx));
-      if (e == hipSuccess) e = hipMalloc((void**)&bh, 2 * M * sizeof(cplx));
-      if (e == hipSuccess) e = hipMalloc((void**)&tmp, 4 * M * sizeof(cplx));
-      if (e == hipSuccess) {
-        hipLaunchKernelGGL(chirp_table, dim3(blocks(N)), dim3(256), 0, s, w, N);
-        hipLaunchKernelGGL(chirp_b, dim3(blocks(2 * M)), dim3(256), 0, s, tmp, w, N, M);
-        e = hipGetLastError();
-      }
-      if (e == hipSuccess) {
-        st = fft_to_spec(M, 2, tmp, bh, tmp + 2 * M, s, c.T);  // column-major, as bs_mul
-        if (st == JW_OK) e = hipStreamSynchronize(s);
-      }
-      if (tmp) (void)hipFree(tmp);
-      if (e != hipSuccess || st != JW_OK) {
-        if (w) (void)hipFree(w);
-        if (bh) (void)hipFree(bh);
-        return st != JW_OK ? st
-                           : fail(JW_ERR_DEVICE, "chirp-z tables for N=%ld: %s", N,
-                                  hipGetErrorString(e));
-      }
-      c.w = w;
-      c.bh[0] = bh;
-      c.bh[1] = bh + M;
-      it = g_bs.emplace(std::make_pair(dev, N), c).first;
-    }
-    *B = it->second;
-  }
+  B->N = N;
+  B->M = 1;
+  while (B->M < 2 * N - 1) B->M <<= 1;
+  const long M = B->M;
+  int st = fft::tables(M, &B->T);
+  if (st != JW_OK) return st;
+  const void* tab = nullptr;
+  st = cached_table(g_bs, std::make_pair(dev, N), (size_t)(N + 2 * M) * sizeof(cplx), mem, s, &tab,
+                    [&](void* d) -> int {
+                      cplx* w = (cplx*)d;
+                      cplx* bh = w + N;
+                      cplx* tmp = nullptr;
+                      JW_HIP_TRY(mem.alloc(&tmp, (size_t)4 * M * sizeof(cplx)));
+                      hipLaunchKernelGGL(chirp_table, dim3(blocks(N)), dim3(256), 0, s, w, N);
+                      hipLaunchKernelGGL(chirp_b, dim3(blocks(2 * M)), dim3(256), 0, s, tmp, w, N, M);
+                      JW_HIP_TRY(hipGetLastError());
+                      // column-major, as bs_mul reads it
+                      return fft_to_spec(M, 2, tmp, bh, tmp + 2 * M, s, B->T);
+                    });
+  if (st != JW_OK) return st;
+  B->w = (const cplx*)tab;
+  B->bh[0] = (const cplx*)tab + N;
+  B->bh[1] = (const cplx*)tab + N + M;
   B->ws_items = max_items;
-  JW_HIP_TRY(mem.alloc(&B->ws, (size_t)3 * max_items * B->M * sizeof(cplx)));
+  JW_HIP_TRY(mem.alloc(&B->ws, (size_t)3 * max_items * M * sizeof(cplx)));
   return JW_OK;
 }
 
@@ -580,10 +564,7 @@ struct PairKey {
     return std::tie(dev, L, J, N, N1, taps) < std::tie(o.dev, o.L, o.J, o.N, o.N1, o.taps);
   }
 };
-constexpr size_t kPairCacheBytes = 4UL << 30;
-std::mutex g_pair_mu;
-std::map<PairKey, cplx*> g_pair;
-size_t g_pair_bytes = 0;
+DevCache<PairKey> g_pair(4UL << 30);
 
 int build_pair_tables(const ModwtPlan& p, long N, int J, long N1, long N2, const Tables& T,
                       cplx* P, StreamAllocs& mem, hipStream_t s) {
@@ -603,30 +584,12 @@ int pair_tables(const ModwtPlan& p, long N, int J, long N1, long N2, const Table
   JW_HIP_TRY(hipGetDevice(&key.dev));
   key.taps.assign(p.g, p.g + p.L);
   key.taps.insert(key.taps.end(), p.h, p.h + p.L);
-  std::lock_guard<std::mutex> lk(g_pair_mu);
-  auto it = g_pair.find(key);
-  if (it != g_pair.end()) {
-    *P = it->second;
-    return JW_OK;
-  }
-  if (g_pair_bytes + bytes > kPairCacheBytes) {  // cache full: a table for this call only
-    JW_HIP_TRY(mem.alloc(P, bytes));
-    return build_pair_tables(p, N, J, N1, N2, T, *P, mem, s);
-  }
-  cplx* tab = nullptr;
-  JW_HIP_TRY(hipMalloc((void**)&tab, bytes));
-  int st = build_pair_tables(p, N, J, N1, N2, T, tab, mem, s);
-  hipError_t e = st == JW_OK ? hipStreamSynchronize(s) : hipSuccess;
-  if (st != JW_OK || e != hipSuccess) {
-    (void)hipFree(tab);
-    return st != JW_OK ? st
-                       : fail(JW_ERR_DEVICE, "MODWT FFT pair tables for N=%ld: %s", N,
-                              hipGetErrorString(e));
-  }
-  g_pair.emplace(std::move(key), tab);
-  g_pair_bytes += bytes;
-  *P = tab;
-  return JW_OK;
+  const void* tab = nullptr;
+  const int st = cached_table(g_pair, key, bytes, mem, s, &tab, [&](void* d) -> int {
+    return build_pair_tables(p, N, J, N1, N2, T, (cplx*)d, mem, s);
+  });
+  *P = (cplx*)tab;
+  return st;
 }
 
 // signals per chunk: spectra + pass workspace of about 4 GB (HBM holds 288 GB; bigger chunks

@@ -44,7 +44,8 @@ JW_WAVELET_HAAR_ORTH = 1
 # Every symbol include/jwave_hip.h declares (checked by
 # tests/test_capi.py::test_library_exports_every_header_symbol).
 EXPORTS = (
-    "jw_last_error", "jw_version",
+    "jw_last_error", "jw_version", "jw_device_count", "jw_set_device", "jw_get_device",
+    "jw_release_caches",
     "jw_modwt_plan_create", "jw_modwt_plan_destroy", "jw_modwt_plan_filters",
     "jw_modwt_forward", "jw_modwt_inverse",
     "jw_fwt_plan_create", "jw_fwt_plan_destroy", "jw_fwt_forward", "jw_fwt_reverse",
@@ -81,6 +82,11 @@ def lib():
     L.jw_last_error.argtypes = []
     L.jw_version.restype = ctypes.c_char_p
     L.jw_version.argtypes = []
+    L.jw_device_count.argtypes = [ctypes.POINTER(i)]
+    L.jw_set_device.argtypes = [i]
+    L.jw_get_device.argtypes = [ctypes.POINTER(i)]
+    L.jw_release_caches.argtypes = []
+    L.jw_release_caches.restype = l
     L.jw_modwt_plan_create.argtypes = [ctypes.POINTER(c_dp), c_dp, c_dp, i, i, i]
     L.jw_modwt_plan_destroy.argtypes = [c_dp]
     L.jw_modwt_plan_destroy.restype = None
@@ -110,7 +116,8 @@ def lib():
     L.jw_cwt_scalogram.argtypes = [c_dp, l, l, c_dp, i, c_dp]
     L.jw_cwt_fft_scalogram.argtypes = [i, c_dp, c_dp, l, c_dp, i, ctypes.c_double, i, c_dp, i, i,
                                        c_dp]
-    non_int = ("jw_last_error", "jw_version", "jw_modwt_plan_destroy", "jw_fwt_plan_destroy")
+    non_int = ("jw_last_error", "jw_version", "jw_modwt_plan_destroy", "jw_fwt_plan_destroy",
+               "jw_release_caches")
     for name in EXPORTS:
         if name not in non_int:
             getattr(L, name).restype = ctypes.c_int
@@ -134,3 +141,20 @@ def check(status):
     if status == JW_ERR_UNSUPPORTED:
         raise NotImplementedError(msg)
     raise JWaveError(f"HIP engine error {status}: {msg}")
+
+
+def set_device(ordinal):
+    """jw_set_device: the calling thread's device for every later call."""
+    check(lib().jw_set_device(int(ordinal)))
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    check(lib().jw_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def release_caches():
+    """jw_release_caches: free every cached device table (MODWTTransform.clearFilterCache's
+    device-side counterpart); returns the bytes freed."""
+    return int(lib().jw_release_caches())

@@ -10,6 +10,7 @@
 #include "jwave_oracle.h"
 
 #include <math.h>
+#include <quadmath.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -225,6 +226,25 @@ void jwo_modwt_inverse_direct(const double* coeffs, long N, int J, const double*
 static int g_exact_twiddles = 0;
 void jwo_set_exact_twiddles(int on) { g_exact_twiddles = on; }
 
+/* Math.cos / Math.sin (:189-190, :269-271) restated as the correctly rounded values: Java
+ * specifies them to 1 ulp and its implementations round correctly for all but a vanishing
+ * fraction of arguments, while glibc's sin / cos / sincos each misround some (e.g. the chirp
+ * of n = 2049).  Long double first; the quad-precision value where that cannot decide. */
+static double cr_round(long double v, __float128 (*slow)(__float128), double x) {
+  double d = (double)v;
+  if (v == 0.0L || !isfinite(d)) return d;
+  long double err = ldexpl(1.0L, ilogbl(v) - 63 + 4);
+  long double ld = d;
+  long double hi = (ld + (long double)nextafter(d, INFINITY)) / 2;
+  long double lo = (ld + (long double)nextafter(d, -INFINITY)) / 2;
+  if (fabsl(v - hi) > err && fabsl(v - lo) > err) return d;
+  return (double)slow((__float128)x);
+}
+static void java_sincos(double x, double* s, double* c) {
+  *s = cr_round(sinl((long double)x), sinq, x);
+  *c = cr_round(cosl((long double)x), cosq, x);
+}
+
 static void fft_ct(double* x, long n, int inverse, int normalize) {
   int p = 0;
   while ((1L << p) < n) p++;
@@ -239,7 +259,8 @@ static void fft_ct(double* x, long n, int inverse, int normalize) {
   }
   for (long size = 2; size <= n; size *= 2) { /* :188-202 */
     double angle = 2 * JAVA_PI / (double)size * (inverse ? 1 : -1);
-    double wr = cos(angle), wi = sin(angle);
+    double wr, wi;
+    java_sincos(angle, &wi, &wr);
     long half = size / 2;
     for (long start = 0; start < n; start += size) {
       double nr = 1, ni = 0; /* wn = (1,0) */
@@ -277,8 +298,7 @@ static void fft_bluestein(double* x, long n, int inverse) {
   double* b = (double*)calloc(2 * m, sizeof(double));
   for (long i = 0; i < n; i++) {
     double angle = JAVA_PI * (double)i * (double)i / (double)n * (inverse ? 1 : -1);
-    chirp[2 * i] = cos(angle);
-    chirp[2 * i + 1] = sin(angle);
+    java_sincos(angle, &chirp[2 * i + 1], &chirp[2 * i]);
   }
   for (long i = 0; i < n; i++) { /* a[i] = x[i].mul(chirp[i]) */
     double xr = x[2 * i], xi = x[2 * i + 1], cr = chirp[2 * i], ci = chirp[2 * i + 1];

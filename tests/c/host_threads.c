@@ -14,7 +14,7 @@
 #include "jwave_oracle.h"
 
 #define THREADS 8
-#define ITERS 6
+#define ITERS 10
 
 /* Daubechies-2-like 8-tap scaling filter and its quadrature mirror (any filter pair serves:
  * the check is engine vs oracle with the same taps). */
@@ -25,6 +25,7 @@ static double kWav[8];
 
 static const jw_modwt_plan* g_plan;
 static double g_g[8], g_h[8];
+static int g_device = -1; /* argv[1]: every thread jw_set_device()s it first */
 
 typedef struct {
   int id;
@@ -36,28 +37,49 @@ static int same_bits(const double* a, const double* b, size_t n) {
   return memcmp(a, b, n * sizeof(double)) == 0;
 }
 
+/* Every 5th call runs ConvolutionMethod.AUTO (JWave's default; power-of-two n, so the FFT
+ * levels run the reference's own FFT and stay bit-exact against the oracle's AUTO path), and
+ * thread 0 calls jw_release_caches() every 10th iteration while the others run -- the
+ * MODWTThreadSafetyTest pattern with clearFilterCache() (MODWTThreadSafetyTest.java:53-54). */
 static void* worker(void* arg) {
   job* jb = (job*)arg;
+  if (g_device >= 0 && jw_set_device(g_device) != JW_OK) {
+    jb->failures++;
+    snprintf(jb->msg, sizeof jb->msg, "thread %d: jw_set_device(%d): %s", jb->id, g_device,
+             jw_last_error());
+    return NULL;
+  }
   for (int it = 0; it < ITERS; ++it) {
-    const long n = 4096 + 1000L * jb->id + 37L * it; /* distinct staging sizes per call */
+    const int autom = it % 5 == 4;
+    const long n = autom ? 4096L << (it % 3) : 4096 + 1000L * jb->id + 37L * it; /* distinct sizes */
     const int J = 3 + (jb->id + it) % 6;
     const int B = 1 + (it % 3);
+    const int method = autom ? JW_CONV_AUTO : JW_CONV_DIRECT;
+    if (jb->id == 0 && it % 10 == 9 && jw_release_caches() < 0) {
+      jb->failures++;
+      snprintf(jb->msg, sizeof jb->msg, "jw_release_caches failed: %s", jw_last_error());
+    }
     double* x = malloc(sizeof(double) * n * B);
     double* c = malloc(sizeof(double) * n * (J + 1) * B);
     double* xr = malloc(sizeof(double) * n * B);
     double* cref = malloc(sizeof(double) * n * (J + 1));
     double* xref = malloc(sizeof(double) * n);
     for (int b = 0; b < B; ++b) jwo_fill_uniform(x + (size_t)b * n, n, 1000L * jb->id + 10L * it + b);
-    int st = jw_modwt_forward(g_plan, x, c, n, J, B, JW_CONV_DIRECT, JW_HOST, NULL);
-    if (st == JW_OK) st = jw_modwt_inverse(g_plan, c, xr, n, J, B, JW_CONV_DIRECT, JW_HOST, NULL);
+    int st = jw_modwt_forward(g_plan, x, c, n, J, B, method, JW_HOST, NULL);
+    if (st == JW_OK) st = jw_modwt_inverse(g_plan, c, xr, n, J, B, method, JW_HOST, NULL);
     if (st != JW_OK) {
       jb->failures++;
       snprintf(jb->msg, sizeof jb->msg, "thread %d iter %d: status %d (%s)", jb->id, it, st,
                jw_last_error());
     } else {
       for (int b = 0; b < B; ++b) {
-        jwo_modwt_forward_direct_nz(x + (size_t)b * n, n, J, g_g, g_h, 8, cref);
-        jwo_modwt_inverse_direct_nz(cref, n, J, g_g, g_h, 8, xref);
+        if (autom) {
+          jwo_modwt_forward_auto(x + (size_t)b * n, n, J, g_g, g_h, 8, 4096, cref);
+          jwo_modwt_inverse_auto(c + (size_t)b * n * (J + 1), n, J, g_g, g_h, 8, 4096, xref);
+        } else {
+          jwo_modwt_forward_direct_nz(x + (size_t)b * n, n, J, g_g, g_h, 8, cref);
+          jwo_modwt_inverse_direct_nz(cref, n, J, g_g, g_h, 8, xref);
+        }
         if (!same_bits(c + (size_t)b * n * (J + 1), cref, (size_t)n * (J + 1)) ||
             !same_bits(xr + (size_t)b * n, xref, (size_t)n)) {
           jb->failures++;
@@ -71,7 +93,8 @@ static void* worker(void* arg) {
   return NULL;
 }
 
-int main(void) {
+int main(int argc, char** argv) {
+  if (argc > 1) g_device = atoi(argv[1]);
   for (int k = 0; k < 8; ++k) kWav[k] = (k & 1 ? -1.0 : 1.0) * kScal[7 - k];
   jw_modwt_plan* p = NULL;
   if (jw_modwt_plan_create(&p, kScal, kWav, 8, 4096, JW_ARITH_STRICT) != JW_OK) {
@@ -101,6 +124,7 @@ int main(void) {
     if (jobs[i].failures) fprintf(stderr, "%s\n", jobs[i].msg);
   }
   jw_modwt_plan_destroy(p);
-  printf("host_threads: %d threads x %d calls, %d failures\n", THREADS, ITERS, fails);
+  printf("host_threads: %d threads x %d calls (device %d), %d failures\n", THREADS, ITERS,
+         g_device, fails);
   return fails ? 1 : 0;
 }

@@ -330,3 +330,22 @@ def test_cwt_result_abi_validation():
     assert L.jw_cwt_magnitude(p, 0, o, 0, None) == 0
     assert L.jw_cwt_scalogram(p, 0, 4, o, 1, None) == 0
     assert L.jw_cwt_magnitude(None, 4, o, 0, None) == -1
+
+
+def test_device_ordinal_errors():
+    # jw_set_device: the C-ABI's device choice for JVM callers that fan out over GPUs
+    # (ParallelTransform.java:83-86 style); invalid ordinals are IllegalArgumentException
+    lib = _native.lib()
+    n = _native.device_count()
+    assert n >= 0
+    assert lib.jw_set_device(-1) == _native.JW_ERR_ILLEGAL_ARGUMENT
+    assert "must be >= 0" in _native.last_error()
+    assert lib.jw_set_device(n) == _native.JW_ERR_ILLEGAL_ARGUMENT
+    assert f"out of range: {n} HIP device(s) visible" in _native.last_error()
+    with pytest.raises(IllegalArgumentException):
+        _native.set_device(1 << 20)
+
+
+def test_release_caches_without_calls():
+    # nothing cached yet in this process (no GPU here): frees nothing, never fails
+    assert _native.release_caches() >= 0

@@ -239,3 +239,43 @@ def test_row4096_kernels_bit_exact(wname, monkeypatch):
         assert bits_equal(fm.forward(x, lvl), yf), lvl
         assert bits_equal(fm.reverse(ref, lvl), rf), lvl
         monkeypatch.delenv("JW_FWT_ROW")
+
+
+@pytest.mark.parametrize("arith", ["strict", "fma"])
+def test_cfg4_full_images(arith, device):
+    # BASELINE configs[3] at its own size: FastWaveletTransform(Daubechies8) 2-D forward and
+    # reverse of 4096 x 4096 images, 12 x 12 levels (BasicTransform.java:361-474), two images
+    # of the batched call on HBM (the bench's synthetic inputs, seeds 11 and 12).  STRICT is
+    # bit-exact with the oracle's rows-then-columns restatement; FMA within 1e-10 normwise.
+    import ctypes
+
+    import torch
+    from jwave import _native
+    wv = W.Daubechies8()
+    R, lvl, B = 4096, 12, 2
+    x = torch.empty((B, R, R), dtype=torch.float64, device=device)
+    _native.check(_native.lib().jw_synth_uniform(ctypes.c_void_p(x.data_ptr()), R * R, B, 11, None))
+    f = FastWaveletTransform(wv, arith=arith)
+    y = f.forward2DBatch(x, lvl, lvl)
+    torch.cuda.synchronize()
+    refs = []
+    for b in range(B):
+        xb = orc.fill_uniform(R * R, 11 + b).reshape(R, R)
+        assert bits_equal(x[b].cpu().numpy(), xb)
+        ref = orc.fwt2d_forward(xb, lvl, lvl, wv)
+        got = y[b].cpu().numpy()
+        if arith == "strict":
+            assert bits_equal(got, ref), b
+        else:
+            assert np.max(np.abs(got - ref)) <= 1e-10 * np.max(np.abs(ref)), b
+        refs.append(ref)
+    yr = torch.from_numpy(np.stack(refs)).to(device)
+    xr = f.reverse2DBatch(yr, lvl, lvl)
+    torch.cuda.synchronize()
+    for b in range(B):
+        rref = orc.fwt2d_reverse(refs[b], lvl, lvl, wv)
+        got = xr[b].cpu().numpy()
+        if arith == "strict":
+            assert bits_equal(got, rref), b
+        else:
+            assert np.max(np.abs(got - rref)) <= 1e-10 * np.max(np.abs(rref)), b

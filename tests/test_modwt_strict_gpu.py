@@ -157,3 +157,55 @@ def test_fft_strict_largest_column():
     z = rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n)
     X = FastFourierTransform().forwardComplex(z)
     assert bits_equal(X.view(np.float64), orc.fft(z).view(np.float64))
+
+
+# ---- lengths that are not powers of two: the reference's Bluestein transform (:259-324) ----
+BLUESTEIN = [3, 5, 6, 7, 12, 100, 1000, 2049, 4097, 70001, 1000003]
+
+
+@pytest.mark.parametrize("n", BLUESTEIN)
+def test_fft_strict_bluestein_bit_exact(n):
+    rng = np.random.default_rng(n)
+    B = 2
+    z = rng.uniform(-1, 1, (B, n)) + 1j * rng.uniform(-1, 1, (B, n))
+    f = FastFourierTransform()
+    X = f.forwardComplex(z)
+    for b in range(B):
+        assert bits_equal(X[b].view(np.float64), orc.fft(z[b]).view(np.float64)), b
+    zr = f.reverseComplex(X)
+    for b in range(B):
+        assert bits_equal(zr[b].view(np.float64), orc.fft(X[b], inverse=True).view(np.float64)), b
+
+
+@pytest.mark.parametrize("wname,n,J", [("Daubechies6", 100, 3), ("Daubechies6", 288, 3),
+                                       ("Daubechies6", 500, 3), ("Daubechies6", 1000, 3),
+                                       ("Haar1", 3, 1), ("Symlet8", 12, 2), ("Daubechies4", 5, 2),
+                                       ("Daubechies4", 4097, 8), ("Daubechies6", 70001, 3),
+                                       ("Symlet8", 3000, 5)])
+def test_auto_bluestein_lengths_bit_exact(wname, n, J):
+    # MODWTInverseTest.java:75-91 lengths and wrap-heavy short ones, JWave's default AUTO: DIRECT
+    # levels where N*M_j <= 4096, the reference's Bluestein FFT convolution elsewhere
+    wv = W.by_name(wname)
+    g, h = ofilters(wv)
+    xs = np.stack([clean_signal(n) + orc.fill_uniform(n, n + b) for b in range(3)])
+    m = MODWTTransform(wv)
+    c = m.forwardMODWT(xs, J)
+    for b in range(3):
+        assert bits_equal(c[b], orc.modwt_forward(xs[b], J, g, h, "auto")), b
+    xr = m.inverseMODWT(c)
+    for b in range(3):
+        assert bits_equal(xr[b], orc.modwt_inverse(c[b], g, h, "auto")), b
+    assert mse(xr, xs) < 1e-10
+
+
+@pytest.mark.parametrize("wname,n,J", [("Daubechies4", 100, 3), ("Symlet8", 7, 2),
+                                       ("Daubechies6", 5000, 4)])
+def test_fft_method_bluestein_bit_exact(wname, n, J):
+    wv = W.by_name(wname)
+    g, h = ofilters(wv)
+    x = orc.fill_uniform(n, 3 * n)
+    m = MODWTTransform(wv)
+    m.setConvolutionMethod(ConvolutionMethod.FFT)
+    c = m.forwardMODWT(x, J)
+    assert bits_equal(c, orc.modwt_forward(x, J, g, h, "fft"))
+    assert bits_equal(m.inverseMODWT(c), orc.modwt_inverse(c, g, h, "fft"))
