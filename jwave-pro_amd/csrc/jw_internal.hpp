@@ -10,6 +10,7 @@
 #include <shared_mutex>
 #include <string>
 #include <utility>
+#include <vector>
 
 #include "jwave_hip.h"
 
@@ -48,12 +49,11 @@ class StreamAllocs {
   StreamAllocs(const StreamAllocs&) = delete;
   StreamAllocs& operator=(const StreamAllocs&) = delete;
   ~StreamAllocs() {
-    for (int i = n_ - 1; i >= 0; --i) (void)hipFreeAsync(p_[i], s_);
+    for (size_t i = p_.size(); i-- > 0;) (void)hipFreeAsync(p_[i], s_);
   }
   template <class T>
   hipError_t alloc(T** out, size_t bytes) {
     *out = nullptr;
-    if (n_ == kMax) return hipErrorOutOfMemory;
     hipMemPool_t pool = device_pool();
     if (!pool) return hipErrorOutOfMemory;
     void* p = nullptr;
@@ -65,17 +65,15 @@ class StreamAllocs {
       e = hipMallocFromPoolAsync(&p, bytes, pool, s_);
     }
     if (e == hipSuccess) {
-      p_[n_++] = p;
+      p_.push_back(p);
       *out = (T*)p;
     }
     return e;
   }
 
  private:
-  static constexpr int kMax = 16;
   hipStream_t s_;
-  void* p_[kMax] = {};
-  int n_ = 0;
+  std::vector<void*> p_;
 };
 
 // Calls in flight hold this shared; jw_release_caches() takes it exclusively, so no call is

@@ -229,12 +229,13 @@ int forward_cols(const ModwtPlan& p, const bool* fft, const cplx* F, const Tw& t
       });
       if (st != JW_OK) break;
     }
-    // forward pass 2, X . F_h / X . F_g, inverse pass 1 of both
+    // forward pass 2, X . F_h / X . F_g, inverse pass 1 of each (one filter per item: a
+    // workgroup holding both products needed ~210 VGPRs, half the waves)
     st = with_big_lc(g.C, [&](auto LCc) -> int {
       constexpr int LC = decltype(LCc)::value;
-      return launch_grid<LC>(kp2p<LC, 2, RowsC, FwdMid, OutF>, (g.R / Geo<LC>::T) * nb, s,
-                             RowsC{Z, N}, FwdMid{spec_h(F, N, j), spec_g(F, N, j)},
-                             OutF{Zi, N, nb * N}, g.rbits, nb, twf.p2, twi.p1);
+      return launch_grid<LC>(kp2p<LC, 1, ZPair, FwdMid, OutPair>, (g.R / Geo<LC>::T) * 2 * nb, s,
+                             ZPair{Z, N}, FwdMid{spec_h(F, N, j), spec_g(F, N, j)},
+                             OutPair{Zi, N, nb * N}, g.rbits, 2 * nb, twf.p2, twi.p1);
     });
     if (st != JW_OK) break;
     const double inv_n = 1.0 / (double)N;

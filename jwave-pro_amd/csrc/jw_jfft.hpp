@@ -23,9 +23,10 @@
 // The pass-2 twiddles are stored transposed (Tw2[l][m] = Tw[m R + l]) so that the lanes of one
 // column read consecutive entries.  Short transforms (n <= 4096) run whole in one "column".
 //
-// A column of LC points is held by LC/EPT threads with EPT = min(16, LC) points each; a
+// A column of LC points is held by LC/EPT threads with EPT = min(8, LC) points each; a
 // workgroup of 256 threads holds T = 256 EPT / LC columns in LDS (padded: one slot per 16
-// points, one per column).  Stages run in register groups of up to 4 (radix 16).
+// points, one per column).  Stages run in register groups of up to 3 (radix 8): at <= 128
+// VGPRs four waves per SIMD stay resident (16 points per thread needed ~200).
 #pragma once
 #include "jw_internal.hpp"
 
@@ -34,6 +35,7 @@ namespace jf {
 
 using cplx = double2;
 constexpr int kNT = 256;
+constexpr int kEPT = 8;  // points per thread (radix-8 register groups)
 
 __host__ __device__ constexpr int ilog2(long v) {
   int r = 0;
@@ -44,7 +46,8 @@ __host__ __device__ constexpr int ilog2(long v) {
 template <int LC>
 struct Geo {
   static constexpr int LOG = ilog2(LC);
-  static constexpr int EPT = LC < 16 ? LC : 16;
+  // (a 4096-point column needs 16 per thread: at most kNT threads per column)
+  static constexpr int EPT = LC < kEPT ? LC : (LC / kNT > kEPT ? LC / kNT : kEPT);
   static constexpr int GMAX = ilog2(EPT);
   static constexpr int TPC = LC / EPT;  // threads per column (divides 64 when <= 64)
   static constexpr int T = kNT / TPC;   // columns per workgroup

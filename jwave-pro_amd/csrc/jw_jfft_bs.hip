@@ -149,9 +149,11 @@ struct BMid {  // a[i].mul(b[i]) (:300-302)
 };
 
 // `items` Bluestein transforms of length n: pre supplies x (before the chirp), post receives
-// the results (both get the tables filled in here).
-int bs_rows(long n, bool inverse, long items, Pre pre, Post post, StreamAllocs& mem,
+// the results (both get the tables filled in here).  Workspaces are this call's own
+// (stream-ordered: released after the kernels queued here have used them).
+int bs_rows(long n, bool inverse, long items, Pre pre, Post post, StreamAllocs& /*caller*/,
             hipStream_t s) {
+  StreamAllocs mem(s);
   BsTab T;
   int st = bs_tables(n, inverse, &T, mem, s);
   if (st != JW_OK) return st;

@@ -114,11 +114,28 @@ struct PowPost {  // result[i].mul(1.0 / n).getReal() (:207-211, :781-783)
   double inv_n;
   __device__ double operator()(int, long, long, cplx v) const { return v.x * inv_n; }
 };
-// forward level: signalFFT[i].mul(filterFFT[i]), f = 0 -> h_j (W_j), f = 1 -> g_j (V_j) (:775-778)
+// forward level, one filter per item: item 2 sig + f reads signal sig's spectrum (Z rows of
+// sig) and takes signalFFT[i].mul(filterFFT[i]) with f = 0 -> h_j (W_j), 1 -> g_j (V_j)
+// (:775-778).  The two items of a signal are adjacent, so they run back to back on one XCD
+// (tile_item) and the second one's Z column tile comes from L2.
+struct ZPair {
+  const cplx* p;
+  long st;
+  __device__ cplx operator()(long it, long i) const { return p[(it >> 1) * st + i]; }
+};
 struct FwdMid {
   const cplx* fh;
   const cplx* fg;
-  __device__ cplx operator()(int f, long, long i, cplx x) const { return jmul(x, (f ? fg : fh)[i]); }
+  __device__ cplx operator()(int, long it, long i, cplx x) const {
+    return jmul(x, ((it & 1) ? fg : fh)[i]);
+  }
+};
+struct OutPair {  // item 2 sig + f -> stream f's row sig
+  cplx* p;
+  long st, fst;
+  __device__ void operator()(int, long it, long j, cplx v) const {
+    p[(it & 1) * fst + (it >> 1) * st + j] = v;
+  }
 };
 // adjoint: signalFFT[i].mul(filterFFT[i].conjugate()) (:820-824); items [0, nb) are V_j (g_j),
 // [nb, 2 nb) are W_j (h_j)
