@@ -24,7 +24,7 @@
 // column read consecutive entries.  Short transforms (n <= 4096) run whole in one "column".
 //
 // A column of LC points is held by LC/EPT threads with EPT = min(8, LC) points each; a
-// workgroup of 256 threads holds T = 256 EPT / LC columns in LDS (padded: one slot per 16
+// workgroup of 512 threads holds T = 512 EPT / LC columns in LDS (padded: one slot per 16
 // points, one per column).  Stages run in register groups of up to 3 (radix 8): at <= 128
 // VGPRs four waves per SIMD stay resident (16 points per thread needed ~200).
 #pragma once
@@ -34,7 +34,7 @@ namespace jw {
 namespace jf {
 
 using cplx = double2;
-constexpr int kNT = 256;
+constexpr int kNT = 512;
 constexpr int kEPT = 8;  // points per thread (radix-8 register groups)
 
 __host__ __device__ constexpr int ilog2(long v) {
