@@ -3,6 +3,9 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <condition_variable>
+#include <deque>
+#include <thread>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -113,75 +116,180 @@ int floor_log2(long n) {
 
 bool is_binary(long n) { return n > 0 && (n & (n - 1)) == 0; }  // MathToolKit.isBinary :185-188
 
-// JW_HOST staging (what a JNI crossing with double[] uses): per host thread and device, two
-// pinned bounce buffers that pipeline the pageable-memory copies (memcpy of chunk k+1 beside
-// the DMA of chunk k) and a private non-blocking stream when the caller passes none (threads
-// never meet on the null stream).  The HBM copies of the caller's arrays come from the
-// library's memory pool per call (stream-ordered: no hipMalloc / hipFree, which synchronise
-// the device and would serialise concurrent Java threads).
-constexpr size_t kPinDoubles = (size_t)4 << 20;  // 32 MiB per bounce buffer
+// ---- JW_HOST staging (what a JNI crossing with double[] uses) ----
+// Host copies between the caller's pageable arrays and the pinned bounce buffers run on a
+// small pool of worker threads (one memcpy thread moves ~10 GB/s, PCIe 5 x16 ~50 GB/s per
+// direction); the calling thread takes a share too.  Workers: JW_COPY_THREADS, else half of
+// OMP_NUM_THREADS (the GPU box's per-GPU CPU share is 16) or of the hardware threads, <= 8.
+class CopyPool {
+ public:
+  static CopyPool& get() {
+    static CopyPool* p = new CopyPool();  // never destroyed: detached workers outlive main
+    return *p;
+  }
+  void copy(void* dst, const void* src, size_t bytes) {
+    const int parts = bytes >= (4u << 20) ? workers_ + 1 : 1;
+    if (parts == 1) {
+      std::memcpy(dst, src, bytes);
+      return;
+    }
+    const size_t per = ((bytes + parts - 1) / parts + 4095) & ~(size_t)4095;
+    std::atomic<int> left{0};
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (int i = 1; i < parts; ++i) {
+        const size_t off = per * (size_t)i;
+        if (off >= bytes) break;
+        left.fetch_add(1, std::memory_order_relaxed);
+        q_.push_back(Job{(char*)dst + off, (const char*)src + off, std::min(per, bytes - off),
+                         &left});
+      }
+    }
+    cv_.notify_all();
+    std::memcpy(dst, src, std::min(per, bytes));
+    while (left.load(std::memory_order_acquire) > 0) {  // help, then wait for our parts
+      Job j;
+      if (pop(&j)) {
+        run(j);
+      } else {
+        std::this_thread::yield();
+      }
+    }
+  }
+
+ private:
+  struct Job {
+    char* d;
+    const char* s;
+    size_t n;
+    std::atomic<int>* left;
+  };
+  CopyPool() {
+    int t = 0;
+    if (const char* e = std::getenv("JW_COPY_THREADS")) {
+      workers_ = std::max(0, std::atoi(e) - 1);
+    } else {
+      if (const char* o = std::getenv("OMP_NUM_THREADS")) t = std::atoi(o);
+      if (t <= 0) t = (int)std::thread::hardware_concurrency();
+      workers_ = std::min(7, std::max(0, t / 2 - 1));
+    }
+    for (int i = 0; i < workers_; ++i) std::thread([this] { loop(); }).detach();
+  }
+  bool pop(Job* j) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (q_.empty()) return false;
+    *j = q_.front();
+    q_.pop_front();
+    return true;
+  }
+  static void run(const Job& j) {
+    std::memcpy(j.d, j.s, j.n);
+    j.left->fetch_sub(1, std::memory_order_release);
+  }
+  void loop() {
+    for (;;) {
+      Job j;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [this] { return !q_.empty(); });
+        j = q_.front();
+        q_.pop_front();
+      }
+      run(j);
+    }
+  }
+  int workers_ = 0;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Job> q_;
+};
+
+// Per host thread and device: a private non-blocking stream when the caller passes none
+// (threads never meet on the null stream), one copy stream per direction, and two pinned
+// bounce buffers per direction (memcpy of chunk k+1 beside the DMA of chunk k).  The HBM copies
+// of the caller's arrays come from the library's memory pool per call.
+// doubles per bounce buffer: 32 MiB (JW_PIN_MB for A/B runs)
+size_t pin_doubles() {
+  static const size_t v = [] {
+    const char* e = std::getenv("JW_PIN_MB");
+    const long mb = e ? std::atol(e) : 32;
+    return (size_t)std::max(1L, mb) << 17;
+  }();
+  return v;
+}
 
 struct HostStage {
   int dev = -1;
-  hipStream_t own = nullptr;
-  double* pin[2] = {nullptr, nullptr};
-  hipEvent_t ev[2] = {nullptr, nullptr};
+  hipStream_t own = nullptr, h2d = nullptr, d2h = nullptr;
+  double* pin_in[2] = {nullptr, nullptr};
+  double* pin_out[2] = {nullptr, nullptr};
+  hipEvent_t ev_in[2] = {}, ev_out[2] = {};           // bounce buffer reuse
+  hipEvent_t loaded[2] = {}, done[2] = {}, drained[2] = {};  // sub-batch pipeline
 
   ~HostStage() {
     if (dev < 0) return;
     (void)hipSetDevice(dev);
-    if (own) (void)hipStreamSynchronize(own);
+    for (hipStream_t s : {own, h2d, d2h})
+      if (s) (void)hipStreamSynchronize(s);
     for (int i = 0; i < 2; ++i) {
-      if (pin[i]) (void)hipHostFree(pin[i]);
-      if (ev[i]) (void)hipEventDestroy(ev[i]);
+      if (pin_in[i]) (void)hipHostFree(pin_in[i]);
+      if (pin_out[i]) (void)hipHostFree(pin_out[i]);
+      for (hipEvent_t e : {ev_in[i], ev_out[i], loaded[i], done[i], drained[i]})
+        if (e) (void)hipEventDestroy(e);
     }
-    if (own) (void)hipStreamDestroy(own);
+    for (hipStream_t s : {own, h2d, d2h})
+      if (s) (void)hipStreamDestroy(s);
   }
 
   int init(int device) {
     dev = device;
-    JW_HIP_TRY(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
+    for (hipStream_t* s : {&own, &h2d, &d2h})
+      JW_HIP_TRY(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
     for (int i = 0; i < 2; ++i) {
-      JW_HIP_TRY(hipHostMalloc((void**)&pin[i], kPinDoubles * sizeof(double),
+      JW_HIP_TRY(hipHostMalloc((void**)&pin_in[i], pin_doubles() * sizeof(double),
                                hipHostMallocDefault));
-      JW_HIP_TRY(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+      JW_HIP_TRY(hipHostMalloc((void**)&pin_out[i], pin_doubles() * sizeof(double),
+                               hipHostMallocDefault));
+      for (hipEvent_t* e : {&ev_in[i], &ev_out[i], &loaded[i], &done[i], &drained[i]})
+        JW_HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
     return JW_OK;
   }
 
-  // host -> HBM through the bounce buffers; returns when the host buffer may be reused
-  int put(double* dst, const double* src, size_t n, hipStream_t s) {
-    for (size_t off = 0, k = 0; off < n; off += kPinDoubles, ++k) {
-      const size_t c = std::min(kPinDoubles, n - off);
+  // host -> HBM through the bounce buffers on stream cs; returns when the host buffer may be
+  // reused (the last DMAs may still be in flight on cs)
+  int put(double* dst, const double* src, size_t n, hipStream_t cs) {
+    for (size_t off = 0, k = 0; off < n; off += pin_doubles(), ++k) {
+      const size_t c = std::min(pin_doubles(), n - off);
       const int b = (int)(k & 1);
-      JW_HIP_TRY(hipEventSynchronize(ev[b]));  // this buffer's previous DMA has landed
-      std::memcpy(pin[b], src + off, c * sizeof(double));
-      JW_HIP_TRY(hipMemcpyAsync(dst + off, pin[b], c * sizeof(double), hipMemcpyHostToDevice, s));
-      JW_HIP_TRY(hipEventRecord(ev[b], s));
+      JW_HIP_TRY(hipEventSynchronize(ev_in[b]));  // this buffer's previous DMA has landed
+      CopyPool::get().copy(pin_in[b], src + off, c * sizeof(double));
+      JW_HIP_TRY(hipMemcpyAsync(dst + off, pin_in[b], c * sizeof(double), hipMemcpyHostToDevice, cs));
+      JW_HIP_TRY(hipEventRecord(ev_in[b], cs));
     }
     return JW_OK;
   }
 
-  // HBM -> host after the work queued on s; DMA of chunk k overlaps the memcpy of chunk k-1
-  int get(double* dst, const double* src, size_t n, hipStream_t s) {
+  // HBM -> host after the work queued on cs; DMA of chunk k overlaps the host copy of k-1
+  int get(double* dst, const double* src, size_t n, hipStream_t cs) {
     size_t prev_off = 0, prev_c = 0;
     int prev_b = -1;
-    for (size_t off = 0, k = 0; off < n; off += kPinDoubles, ++k) {
-      const size_t c = std::min(kPinDoubles, n - off);
+    for (size_t off = 0, k = 0; off < n; off += pin_doubles(), ++k) {
+      const size_t c = std::min(pin_doubles(), n - off);
       const int b = (int)(k & 1);
-      JW_HIP_TRY(hipMemcpyAsync(pin[b], src + off, c * sizeof(double), hipMemcpyDeviceToHost, s));
-      JW_HIP_TRY(hipEventRecord(ev[b], s));
+      JW_HIP_TRY(hipMemcpyAsync(pin_out[b], src + off, c * sizeof(double), hipMemcpyDeviceToHost, cs));
+      JW_HIP_TRY(hipEventRecord(ev_out[b], cs));
       if (prev_b >= 0) {
-        JW_HIP_TRY(hipEventSynchronize(ev[prev_b]));
-        std::memcpy(dst + prev_off, pin[prev_b], prev_c * sizeof(double));
+        JW_HIP_TRY(hipEventSynchronize(ev_out[prev_b]));
+        CopyPool::get().copy(dst + prev_off, pin_out[prev_b], prev_c * sizeof(double));
       }
       prev_off = off;
       prev_c = c;
       prev_b = b;
     }
     if (prev_b >= 0) {
-      JW_HIP_TRY(hipEventSynchronize(ev[prev_b]));
-      std::memcpy(dst + prev_off, pin[prev_b], prev_c * sizeof(double));
+      JW_HIP_TRY(hipEventSynchronize(ev_out[prev_b]));
+      CopyPool::get().copy(dst + prev_off, pin_out[prev_b], prev_c * sizeof(double));
     }
     return JW_OK;
   }
@@ -209,30 +317,79 @@ int check_where(int where) {
   return JW_OK;
 }
 
+// Runs f(din, dout, items, s) over `items` independent items (signals, images, lines) of
+// in_per doubles in and out_per doubles out.  JW_DEVICE: the caller's HBM pointers, async on
+// the caller's stream.  JW_HOST: staged through HBM in sub-batches of ~128 MiB, pipelined over
+// three streams -- the host->HBM copy of sub-batch k+1 and the HBM->host copy of k-1 beside the
+// compute of k -- and synchronised before returning.
+constexpr size_t kSubDoubles = (size_t)16 << 20;  // 128 MiB of input + output per sub-batch
+
 template <class F>
-int run(int where, void* stream, const double* in, size_t nin, double* out, size_t nout, F&& f) {
+int run_items(int where, void* stream, const double* in, size_t in_per, double* out,
+              size_t out_per, long items, F&& f) {
   std::shared_lock<std::shared_mutex> in_flight(api_mutex());
   int dev = 0;
   JW_HIP_TRY(hipGetDevice(&dev));
   note_device_used(dev);
   hipStream_t s = (hipStream_t)stream;
-  if (where == JW_DEVICE) return f(in, out, s);
+  if (where == JW_DEVICE) return f(in, out, items, s);
   HostStage* hs = nullptr;
   int st = host_stage(&hs);
   if (st != JW_OK) return st;
   if (!s) s = hs->own;
-  double *din = nullptr, *dout = nullptr;
+  const size_t per = std::max<size_t>(1, in_per + out_per);
+  const long sub = std::max(1L, std::min<long>(items, (long)(kSubDoubles / per)));
+  const long nsub = (items + sub - 1) / sub;
+  hipError_t e1 = hipSuccess, e2 = hipSuccess, e3 = hipSuccess;
   {
     StreamAllocs mem(s);
-    JW_HIP_TRY(mem.alloc(&din, nin * sizeof(double)));
-    JW_HIP_TRY(mem.alloc(&dout, nout * sizeof(double)));
-    if ((st = hs->put(din, in, nin, s)) == JW_OK) st = f(din, dout, s);
-    if (st == JW_OK) st = hs->get(out, dout, nout, s);
-  }  // freed in stream order
-  const hipError_t e = hipStreamSynchronize(s);
+    double *din[2] = {}, *dout[2] = {};
+    for (int b = 0; b < (nsub > 1 ? 2 : 1); ++b) {
+      JW_HIP_TRY(mem.alloc(&din[b], (size_t)sub * in_per * sizeof(double) + 8));
+      JW_HIP_TRY(mem.alloc(&dout[b], (size_t)sub * out_per * sizeof(double) + 8));
+    }
+    auto count = [&](long k) { return std::min(sub, items - k * sub); };
+    auto put = [&](long k) -> int {  // din[k&1] is free once f(k-2) has run
+      const int b = (int)(k & 1);
+      if (k >= 2) JW_HIP_TRY(hipStreamWaitEvent(hs->h2d, hs->done[b], 0));
+      int r = hs->put(din[b], in + (size_t)k * sub * in_per, (size_t)count(k) * in_per, hs->h2d);
+      if (r == JW_OK) JW_HIP_TRY(hipEventRecord(hs->loaded[b], hs->h2d));
+      return r;
+    };
+    auto compute = [&](long k) -> int {  // dout[k&1] is free once sub-batch k-2 has drained
+      const int b = (int)(k & 1);
+      JW_HIP_TRY(hipStreamWaitEvent(s, hs->loaded[b], 0));
+      if (k >= 2) JW_HIP_TRY(hipStreamWaitEvent(s, hs->drained[b], 0));
+      int r = f(din[b], dout[b], count(k), s);
+      if (r == JW_OK) JW_HIP_TRY(hipEventRecord(hs->done[b], s));
+      return r;
+    };
+    auto get = [&](long k) -> int {
+      const int b = (int)(k & 1);
+      JW_HIP_TRY(hipStreamWaitEvent(hs->d2h, hs->done[b], 0));
+      int r = hs->get(out + (size_t)k * sub * out_per, dout[b], (size_t)count(k) * out_per, hs->d2h);
+      if (r == JW_OK) JW_HIP_TRY(hipEventRecord(hs->drained[b], hs->d2h));
+      return r;
+    };
+    st = put(0);
+    if (st == JW_OK) st = compute(0);
+    for (long k = 1; k < nsub && st == JW_OK; ++k) {
+      st = put(k);
+      if (st == JW_OK) st = compute(k);
+      if (st == JW_OK) st = get(k - 1);
+    }
+    if (st == JW_OK) st = get(nsub - 1);
+    // everything queued on the three streams has finished before the workspaces go back to
+    // the pool (in s's order) and before the caller may reuse its arrays
+    e1 = hipStreamSynchronize(hs->h2d);
+    e2 = hipStreamSynchronize(s);
+    e3 = hipStreamSynchronize(hs->d2h);
+  }
+  const hipError_t e4 = hipStreamSynchronize(s);
   if (st != JW_OK) return st;
-  if (e != hipSuccess)
-    return fail(JW_ERR_DEVICE, "hipStreamSynchronize failed: %s", hipGetErrorString(e));
+  for (hipError_t e : {e1, e2, e3, e4})
+    if (e != hipSuccess)
+      return fail(JW_ERR_DEVICE, "hipStreamSynchronize failed: %s", hipGetErrorString(e));
   return JW_OK;
 }
 
@@ -436,19 +593,18 @@ int jw_modwt_forward(const jw_modwt_plan* plan, const double* x, double* coeffs,
   if (st != JW_OK) return st;
   if (st = check_where(where); st != JW_OK) return st;
   if (!x || !coeffs) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
-  const size_t nin = (size_t)n * batch, nout = (size_t)n * batch * (levels + 1);
-  return run(where, stream, x, nin, coeffs, nout,
-             [&](const double* dx, double* dc, hipStream_t s) {
-               bool fft[kMaxModwtLevel + 1] = {};
-               switch (modwt_path(*plan, method, n, levels, fft)) {
-                 case ModwtPath::kStrictLevels:
-                   return modwt_forward_strict_device(*plan, dx, dc, n, levels, batch, fft, s);
-                 case ModwtPath::kPyramid:
-                   return modwt_forward_fft_device(*plan, dx, dc, n, levels, batch, s);
-                 default:
-                   return modwt_forward_device(*plan, dx, dc, n, levels, batch, s);
-               }
-             });
+  return run_items(where, stream, x, (size_t)n, coeffs, (size_t)n * (levels + 1), batch,
+                   [&](const double* dx, double* dc, long nb, hipStream_t s) {
+                     bool fft[kMaxModwtLevel + 1] = {};
+                     switch (modwt_path(*plan, method, n, levels, fft)) {
+                       case ModwtPath::kStrictLevels:
+                         return modwt_forward_strict_device(*plan, dx, dc, n, levels, (int)nb, fft, s);
+                       case ModwtPath::kPyramid:
+                         return modwt_forward_fft_device(*plan, dx, dc, n, levels, (int)nb, s);
+                       default:
+                         return modwt_forward_device(*plan, dx, dc, n, levels, (int)nb, s);
+                     }
+                   });
 }
 
 int jw_modwt_inverse(const jw_modwt_plan* plan, const double* coeffs, double* x, long n,
@@ -468,19 +624,18 @@ int jw_modwt_inverse(const jw_modwt_plan* plan, const double* coeffs, double* x,
   if (st != JW_OK) return st;
   if (st = check_where(where); st != JW_OK) return st;
   if (!x || !coeffs) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
-  const size_t nin = (size_t)n * batch * (levels + 1), nout = (size_t)n * batch;
-  return run(where, stream, coeffs, nin, x, nout,
-             [&](const double* dc, double* dx, hipStream_t s) {
-               bool fft[kMaxModwtLevel + 1] = {};
-               switch (modwt_path(*plan, method, n, levels, fft)) {
-                 case ModwtPath::kStrictLevels:
-                   return modwt_inverse_strict_device(*plan, dc, dx, n, levels, batch, fft, s);
-                 case ModwtPath::kPyramid:
-                   return modwt_inverse_fft_device(*plan, dc, dx, n, levels, batch, s);
-                 default:
-                   return modwt_inverse_device(*plan, dc, dx, n, levels, batch, s);
-               }
-             });
+  return run_items(where, stream, coeffs, (size_t)n * (levels + 1), x, (size_t)n, batch,
+                   [&](const double* dc, double* dx, long nb, hipStream_t s) {
+                     bool fft[kMaxModwtLevel + 1] = {};
+                     switch (modwt_path(*plan, method, n, levels, fft)) {
+                       case ModwtPath::kStrictLevels:
+                         return modwt_inverse_strict_device(*plan, dc, dx, n, levels, (int)nb, fft, s);
+                       case ModwtPath::kPyramid:
+                         return modwt_inverse_fft_device(*plan, dc, dx, n, levels, (int)nb, s);
+                       default:
+                         return modwt_inverse_device(*plan, dc, dx, n, levels, (int)nb, s);
+                     }
+                   });
 }
 
 // ---------------------------------------------------------------- FFT
@@ -497,15 +652,15 @@ static int fft_call(int S, int arith, const double* in, double* out, long n, int
   if (st != JW_OK) return st;
   if (n == 0 || batch == 0) return JW_OK;
   if (!in || !out) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
-  const size_t elems = (size_t)2 * n * batch;
   // STRICT: the reference's own FFT (jw_jfft.hip): radix 2 for powers of two <= 2^24,
   // Bluestein for other n <= 2^23
   const bool strict = arith == JW_ARITH_STRICT && ((n & (n - 1)) == 0 ? n <= (1L << 24)
                                                                       : n <= (1L << 23));
-  return run(where, stream, in, elems, out, elems, [&](const double* di, double* dout, hipStream_t s) {
-    return strict ? fft_strict_device(S, di, dout, n, batch, s)
-                  : fft_device(S, di, dout, n, batch, s);
-  });
+  return run_items(where, stream, in, (size_t)2 * n, out, (size_t)2 * n, batch,
+                   [&](const double* di, double* dout, long nb, hipStream_t s) {
+                     return strict ? fft_strict_device(S, di, dout, n, nb, s)
+                                   : fft_device(S, di, dout, n, nb, s);
+                   });
 }
 
 int jw_fft_forward(const double* in_reim, double* out_reim, long n, int batch, int where,
@@ -588,10 +743,10 @@ int jw_fwt_forward(const jw_fwt_plan* plan, const double* x, double* y, long n, 
   if (st = check_where(where); st != JW_OK) return st;
   if (batch <= 0) return batch == 0 ? JW_OK : fail(JW_ERR_ILLEGAL_ARGUMENT, "negative batch");
   if (!x || !y) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
-  const size_t elems = (size_t)n * batch;
-  return run(where, stream, x, elems, y, elems, [&](const double* dx, double* dy, hipStream_t s) {
-    return fwt_forward_device(*plan, dx, dy, n, level, batch, s);
-  });
+  return run_items(where, stream, x, (size_t)n, y, (size_t)n, batch,
+                   [&](const double* dx, double* dy, long nb, hipStream_t s) {
+                     return fwt_forward_device(*plan, dx, dy, n, level, (int)nb, s);
+                   });
 }
 
 int jw_fwt_reverse(const jw_fwt_plan* plan, const double* y, double* x, long n, int level,
@@ -603,10 +758,10 @@ int jw_fwt_reverse(const jw_fwt_plan* plan, const double* y, double* x, long n, 
   if (st = check_where(where); st != JW_OK) return st;
   if (batch <= 0) return batch == 0 ? JW_OK : fail(JW_ERR_ILLEGAL_ARGUMENT, "negative batch");
   if (!x || !y) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
-  const size_t elems = (size_t)n * batch;
-  return run(where, stream, y, elems, x, elems, [&](const double* dy, double* dx, hipStream_t s) {
-    return fwt_reverse_device(*plan, dy, dx, n, level, batch, s);
-  });
+  return run_items(where, stream, y, (size_t)n, x, (size_t)n, batch,
+                   [&](const double* dy, double* dx, long nb, hipStream_t s) {
+                     return fwt_reverse_device(*plan, dy, dx, n, level, (int)nb, s);
+                   });
 }
 
 // WaveletPacketTransform.forward/reverse validation (WaveletPacketTransform.java:63-72, :122-131).
@@ -630,10 +785,10 @@ int jw_wpt_forward(const jw_fwt_plan* plan, const double* x, double* y, long n, 
   if (st = check_where(where); st != JW_OK) return st;
   if (batch <= 0) return batch == 0 ? JW_OK : fail(JW_ERR_ILLEGAL_ARGUMENT, "negative batch");
   if (!x || !y) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
-  const size_t elems = (size_t)n * batch;
-  return run(where, stream, x, elems, y, elems, [&](const double* dx, double* dy, hipStream_t s) {
-    return wpt_forward_device(*plan, dx, dy, n, level, batch, s);
-  });
+  return run_items(where, stream, x, (size_t)n, y, (size_t)n, batch,
+                   [&](const double* dx, double* dy, long nb, hipStream_t s) {
+                     return wpt_forward_device(*plan, dx, dy, n, level, (int)nb, s);
+                   });
 }
 
 int jw_wpt_reverse(const jw_fwt_plan* plan, const double* y, double* x, long n, int level,
@@ -645,10 +800,10 @@ int jw_wpt_reverse(const jw_fwt_plan* plan, const double* y, double* x, long n, 
   if (st = check_where(where); st != JW_OK) return st;
   if (batch <= 0) return batch == 0 ? JW_OK : fail(JW_ERR_ILLEGAL_ARGUMENT, "negative batch");
   if (!x || !y) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
-  const size_t elems = (size_t)n * batch;
-  return run(where, stream, y, elems, x, elems, [&](const double* dy, double* dx, hipStream_t s) {
-    return wpt_reverse_device(*plan, dy, dx, n, level, batch, s);
-  });
+  return run_items(where, stream, y, (size_t)n, x, (size_t)n, batch,
+                   [&](const double* dy, double* dx, long nb, hipStream_t s) {
+                     return wpt_reverse_device(*plan, dy, dx, n, level, (int)nb, s);
+                   });
 }
 
 int jw_fwt2d_forward(const jw_fwt_plan* plan, const double* x, double* y, int rows, int cols,
@@ -662,10 +817,10 @@ int jw_fwt2d_forward(const jw_fwt_plan* plan, const double* x, double* y, int ro
   if (st = check_where(where); st != JW_OK) return st;
   if (batch <= 0) return batch == 0 ? JW_OK : fail(JW_ERR_ILLEGAL_ARGUMENT, "negative batch");
   if (!x || !y) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
-  const size_t elems = (size_t)rows * cols * batch;
-  return run(where, stream, x, elems, y, elems, [&](const double* dx, double* dy, hipStream_t s) {
-    return fwt2d_forward_device(*plan, dx, dy, rows, cols, lvlM, lvlN, batch, s);
-  });
+  return run_items(where, stream, x, (size_t)rows * cols, y, (size_t)rows * cols,
+                   batch, [&](const double* dx, double* dy, long nb, hipStream_t s) {
+                     return fwt2d_forward_device(*plan, dx, dy, rows, cols, lvlM, lvlN, (int)nb, s);
+                   });
 }
 
 int jw_fwt2d_reverse(const jw_fwt_plan* plan, const double* y, double* x, int rows, int cols,
@@ -679,10 +834,10 @@ int jw_fwt2d_reverse(const jw_fwt_plan* plan, const double* y, double* x, int ro
   if (st = check_where(where); st != JW_OK) return st;
   if (batch <= 0) return batch == 0 ? JW_OK : fail(JW_ERR_ILLEGAL_ARGUMENT, "negative batch");
   if (!x || !y) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
-  const size_t elems = (size_t)rows * cols * batch;
-  return run(where, stream, y, elems, x, elems, [&](const double* dy, double* dx, hipStream_t s) {
-    return fwt2d_reverse_device(*plan, dy, dx, rows, cols, lvlM, lvlN, batch, s);
-  });
+  return run_items(where, stream, y, (size_t)rows * cols, x, (size_t)rows * cols,
+                   batch, [&](const double* dy, double* dx, long nb, hipStream_t s) {
+                     return fwt2d_reverse_device(*plan, dy, dx, rows, cols, lvlM, lvlN, (int)nb, s);
+                   });
 }
 
 // 3-D: BasicTransform.forward/reverse(double[][][], lvlP, lvlQ, lvlR) (:509-659).  The
@@ -700,10 +855,11 @@ int jw_fwt3d_forward(const jw_fwt_plan* plan, const double* x, double* y, int d1
   if (st = check_where(where); st != JW_OK) return st;
   if (batch <= 0) return batch == 0 ? JW_OK : fail(JW_ERR_ILLEGAL_ARGUMENT, "negative batch");
   if (!x || !y) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
-  const size_t elems = (size_t)d1 * d2 * d3 * batch;
-  return run(where, stream, x, elems, y, elems, [&](const double* dx, double* dy, hipStream_t s) {
-    return fwt3d_forward_device(*plan, dx, dy, d1, d2, d3, lvlP, lvlQ, lvlR, batch, s);
-  });
+  const size_t elems = (size_t)d1 * d2 * d3;
+  return run_items(where, stream, x, elems, y, elems, batch,
+                   [&](const double* dx, double* dy, long nb, hipStream_t s) {
+                     return fwt3d_forward_device(*plan, dx, dy, d1, d2, d3, lvlP, lvlQ, lvlR, (int)nb, s);
+                   });
 }
 int jw_fwt3d_reverse(const jw_fwt_plan* plan, const double* y, double* x, int d1, int d2, int d3,
                      int lvlP, int lvlQ, int lvlR, int batch, int where, void* stream) {
@@ -716,10 +872,11 @@ int jw_fwt3d_reverse(const jw_fwt_plan* plan, const double* y, double* x, int d1
   if (st = check_where(where); st != JW_OK) return st;
   if (batch <= 0) return batch == 0 ? JW_OK : fail(JW_ERR_ILLEGAL_ARGUMENT, "negative batch");
   if (!x || !y) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
-  const size_t elems = (size_t)d1 * d2 * d3 * batch;
-  return run(where, stream, y, elems, x, elems, [&](const double* dy, double* dx, hipStream_t s) {
-    return fwt3d_reverse_device(*plan, dy, dx, d1, d2, d3, lvlP, lvlQ, lvlR, batch, s);
-  });
+  const size_t elems = (size_t)d1 * d2 * d3;
+  return run_items(where, stream, y, elems, x, elems, batch,
+                   [&](const double* dy, double* dx, long nb, hipStream_t s) {
+                     return fwt3d_reverse_device(*plan, dy, dx, d1, d2, d3, lvlP, lvlQ, lvlR, (int)nb, s);
+                   });
 }
 
 // ---------------------------------------------------------------- synthetic input
@@ -778,12 +935,11 @@ int jw_cwt_fft(int wavelet, const double* params, const double* x, long n, const
   int st = cwt_fft_check(wavelet, params, n, scales, ns, padding, batch, where);
   if (st != JW_OK) return st;
   if (n == 0 || ns == 0 || batch == 0) return JW_OK;
-  const size_t nin = (size_t)batch * n, nout = (size_t)batch * ns * n * 2;
-  return run(where, stream, x, nin, out_reim, nout,
-             [&](const double* xi, double* o, hipStream_t s) {
-               return cwt_fft_device(wavelet, params, xi, n, scales, ns, sampling_rate, padding,
-                                     o, batch, s);
-             });
+  return run_items(where, stream, x, (size_t)n, out_reim, (size_t)ns * n * 2, batch,
+                   [&](const double* xi, double* o, long nb, hipStream_t s) {
+                     return cwt_fft_device(wavelet, params, xi, n, scales, ns, sampling_rate,
+                                           padding, o, (int)nb, s);
+                   });
 }
 
 // transformFFT(...).getScalogram() with the coefficients kept in a device workspace (signals
@@ -795,9 +951,10 @@ int jw_cwt_fft_scalogram(int wavelet, const double* params, const double* x, lon
   int st = cwt_fft_check(wavelet, params, n, scales, ns, padding, batch, where);
   if (st != JW_OK) return st;
   if (ns == 0 || batch == 0) return JW_OK;
-  const size_t nin = (size_t)batch * n, nout = (size_t)batch * ns;
-  return run(where, stream, x, nin, energy, nout,
-             [&](const double* xi, double* o, hipStream_t s) {
+  return run_items(where, stream, x, (size_t)n, energy, (size_t)ns, batch,
+             [&](const double* xi, double* o, long nbatch, hipStream_t s) {
+               const int batch = (int)nbatch;
+               const size_t nout = (size_t)batch * ns;
                if (n == 0) {  // no time points: zero energy (CWTResult.java:277-284)
                  JW_HIP_TRY(hipMemsetAsync(o, 0, nout * sizeof(double), s));
                  return (int)JW_OK;
@@ -843,12 +1000,11 @@ int jw_cwt_direct(int wavelet, const double* params, const double* x, long n,
   int st = check_where(where);
   if (st != JW_OK) return st;
   if (n == 0 || ns == 0 || batch == 0) return JW_OK;
-  const size_t nin = (size_t)batch * n, nout = (size_t)batch * ns * n * 2;
-  return run(where, stream, x, nin, out_reim, nout,
-             [&](const double* xi, double* o, hipStream_t s) {
-               return cwt_direct_device(wavelet, params, xi, n, scales, ns, sampling_rate, arith,
-                                        o, batch, s);
-             });
+  return run_items(where, stream, x, (size_t)n, out_reim, (size_t)ns * n * 2, batch,
+                   [&](const double* xi, double* o, long nb, hipStream_t s) {
+                     return cwt_direct_device(wavelet, params, xi, n, scales, ns, sampling_rate,
+                                              arith, o, (int)nb, s);
+                   });
 }
 
 // CWTResult.getMagnitude / getPhase / getScalogram (CWTResult.java:94-126, :272-287)
@@ -860,8 +1016,8 @@ static int cwt_elementwise(const double* c, long count, double* out, int where, 
   if (st != JW_OK) return st;
   if (count == 0) return JW_OK;
   if (!c || !out) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
-  return run(where, stream, c, (size_t)count * 2, out, (size_t)count,
-             [&](const double* ci, double* o, hipStream_t s) { return dev(ci, count, o, s); });
+  return run_items(where, stream, c, 2, out, 1, count,
+                   [&](const double* ci, double* o, long k, hipStream_t s) { return dev(ci, k, o, s); });
 }
 
 int jw_cwt_magnitude(const double* coef_reim, long count, double* out, int where, void* stream) {
@@ -881,10 +1037,10 @@ int jw_cwt_scalogram(const double* coef_reim, long rows, long n, double* energy,
   if (st != JW_OK) return st;
   if (rows == 0) return JW_OK;
   if (!coef_reim || !energy) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
-  return run(where, stream, coef_reim, (size_t)rows * n * 2, energy, (size_t)rows,
-             [&](const double* ci, double* o, hipStream_t s) {
-               return cwt_scalogram_device(ci, rows, n, o, s);
-             });
+  return run_items(where, stream, coef_reim, (size_t)n * 2, energy, 1, rows,
+                   [&](const double* ci, double* o, long r, hipStream_t s) {
+                     return cwt_scalogram_device(ci, r, n, o, s);
+                   });
 }
 
 int jw_synth_uniform(double* x_dev, long n, int batch, long seed0, void* stream) {
