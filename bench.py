@@ -97,20 +97,36 @@ def spawn_ranks(n):
     return max(rcs, key=abs)
 
 
-def inv_kernel_name(L, J, n):
-    """Which inverse MODWT kernel the library launches (csrc/jw_modwt_fast.hpp launch_inv and
-    jw_modwt_wave.hpp inv_wave_ok restated): the one-stream-per-wave kernel wherever it fits,
-    the workgroup-shared kernel otherwise or under JW_INV_KERNEL=wg."""
+def inv_kernel_name(L, J, n, arith="fma"):
+    """Which inverse MODWT kernel the library launches (csrc/jw_modwt_fast.hpp launch_inv,
+    jw_modwt_wave2.hpp inv_ok / inv_prefer2 and jw_modwt_wave.hpp inv_wave_ok restated): two
+    outputs per lane (wave2) where it fits and is preferred, else one stream per wave, else the
+    workgroup-shared kernel; JW_INV_KERNEL forces one of them."""
     fast = L in (2, 4, 6, 8, 12, 16, 20) and J <= 10 and 512 <= n < (1 << 27)
     if not fast:
         return "modwt_inv_fused"
-    if os.environ.get("JW_INV_KERNEL", "").startswith("wg") or L % 2 or J < 6:
+    env = os.environ.get("JW_INV_KERNEL", "")
+    if L % 2:
         return "modwt_inv_fast"
     hist = [(L - 1) << (j - 1) for j in range(1, J + 1)]
-    lds = sum(64 + hist[j - 1] for j in range(1, min(J, 5) + 1)) * 16
     rtot = sum((L - 1) * (1 << (j - 7)) + 1 for j in range(7, J + 1))
-    ok = lds <= 20 * 1024 and rtot + max(L // 2, 2) + L // 2 <= 31
-    return "modwt_inv_wave" if ok else "modwt_inv_fast"
+    nx_nz = max(L // 2, 2) + L // 2
+    lds1 = sum(64 + hist[j - 1] for j in range(1, min(J, 5) + 1)) * 16
+    wave1 = J >= 6 and lds1 <= 20 * 1024 and rtot + nx_nz <= 31
+    lds2 = 0
+    for j in range(1, min(J, 5) + 1):
+        d = 1 << (j - 1)
+        nblk = (128 + hist[j - 1]) // d
+        half = ((((nblk + 1) // 2) * d + 7) & ~7) + (d if d < 8 else 0)
+        lds2 += 2 * half * 16
+    wave2 = (n % 2 == 0 and lds2 <= 20 * 1024 and
+             (rtot if J >= 7 else 0) + (nx_nz if J >= 6 else 0) <= 31)
+    prefer2 = J <= 7 or (arith == "fma" and L <= 8)
+    if env == "wg":
+        return "modwt_inv_fast"
+    if wave2 and (env == "wave2" or (env not in ("wave", "wave1") and (prefer2 or not wave1))):
+        return "modwt_inv_wave2"
+    return "modwt_inv_wave" if wave1 else "modwt_inv_fast"
 
 
 def parse():
@@ -624,7 +640,7 @@ def main():
         bytes_per_sample = 8 * (1 + (J + 1))
         per_launch = bytes_per_sample * B * n
         L = len(wv.getScalingDeComposition())
-        name, ms = ((inv_kernel_name(L, J, n), inv_ms) if inv_ms >= fwd_ms
+        name, ms = ((inv_kernel_name(L, J, n, args.arith), inv_ms) if inv_ms >= fwd_ms
                     else ("modwt_fwd_fast", fwd_ms))
         achieved = per_launch / (ms * 1e-3) / 1e9
         traffic = None

@@ -16,6 +16,7 @@
 //    feeds both adjoint sums of a tap and every coefficient is read from HBM once.
 #pragma once
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "jw_internal.hpp"
@@ -594,17 +595,26 @@ constexpr bool inv_fits_topg() {
 }  // namespace fast
 }  // namespace jw
 #include "jw_modwt_wave.hpp"
+#include "jw_modwt_wave2.hpp"
 namespace jw {
 namespace fast {
 
 template <int L, int J, bool FMA>
 int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hipStream_t s) {
+  // The barrier-free kernels are the default wherever they fit: two outputs per lane on the LDS
+  // levels (wave2, N even: 16-byte pairs) where inv_prefer2 says so, else one (wave).
+  // JW_INV_KERNEL = wave2 / wave / wg forces one of them (A/B runs and the parity tests).
+  const char* w = std::getenv("JW_INV_KERNEL");
+  const bool force_wg = w && !std::strcmp(w, "wg");
+  const bool force_w1 = w && (!std::strcmp(w, "wave") || !std::strcmp(w, "wave1"));
+  const bool force_w2 = w && !std::strcmp(w, "wave2");
+  if constexpr (wave2::inv_ok<L, J>()) {
+    if ((N % 2) == 0 && (force_w2 || (!force_wg && !(force_w1 && wave::inv_wave_ok<L, J>()) &&
+                     (wave2::inv_prefer2<L, J, FMA>() || !wave::inv_wave_ok<L, J>()))))
+      return wave2::launch_inv<L, J, FMA>(t, c, x, N, batch, s);
+  }
   if constexpr (wave::inv_wave_ok<L, J>()) {
-    // the barrier-free kernel is the default wherever it fits; JW_INV_KERNEL=wg forces the
-    // workgroup kernel below (A/B runs and its parity tests)
-    const char* w = std::getenv("JW_INV_KERNEL");
-    if (!(w && w[0] == 'w' && w[1] == 'g'))
-      return wave::launch_inv_wave<L, J, FMA>(t, c, x, N, batch, s);
+    if (!force_wg) return wave::launch_inv_wave<L, J, FMA>(t, c, x, N, batch, s);
   }
   constexpr int RF = J >= 7 ? 7 : J + 1;
   const char* e = std::getenv("JW_INV_RING");

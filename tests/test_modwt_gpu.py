@@ -134,11 +134,22 @@ WAVE_CASES = [  # shapes the barrier-free inverse (jw_modwt_wave.hpp) serves: J 
 ]
 
 
-@pytest.mark.parametrize("kernel", ["wave", "wg"])
-@pytest.mark.parametrize("wname,n,J", WAVE_CASES)
+# shapes only the two-outputs-per-lane kernel (jw_modwt_wave2.hpp) serves: J <= 5, its LDS
+# levels alone (top level V_J from HBM as pairs), and long filters
+WAVE2_CASES = [
+    ("Haar1", 600, 1), ("Haar1", 514, 3), ("Daubechies4", 1000, 3), ("Daubechies4", 70002, 5),
+    ("Symlet8", 5000, 5), ("Symlet8", 1 << 16, 6), ("Daubechies20", 2050, 4),
+    ("Daubechies10", 30000, 6), ("Coiflet3", 8194, 7), ("Daubechies2", 1 << 15, 2),
+]
+
+
+@pytest.mark.parametrize("kernel", ["wave", "wave2", "wg"])
+@pytest.mark.parametrize("wname,n,J", WAVE_CASES + WAVE2_CASES)
 def test_inverse_wave_vs_workgroup_bit_exact(wname, n, J, kernel, monkeypatch):
     # one stream per wavefront (no barriers; dilation >= 32 levels in registers, permlane32
-    # swaps for dilation 32) against the workgroup-shared kernel: same bits in both contracts
+    # swaps for dilation 32; wave2: two outputs per lane on the LDS levels) against the
+    # workgroup-shared kernel: same bits in both contracts.  Shapes a kernel does not serve
+    # (odd n for wave2, J < 6 for wave) fall through to the next one.
     wv = W.by_name(wname)
     g, h = ofilters(wv)
     c = orc.modwt_forward(orc.fill_uniform(n, 17 + n), J, g, h, "direct_nz")

@@ -120,5 +120,12 @@ int main() {
   run2<1, 9, 256, 2, false>("forward-like16 1->9", in, out, N, B, 8);
   run2<0, 9, 256, 2, false>("write-only16 9 rows", in, out, N, B, 8);
   run2<0, 1, 256, 4, false>("write-only16 1 row", in, out, N, B * 9, 8);
+  // fewer concurrent streams: more lanes per segment (one stream set per workgroup)
+  run2<9, 1, 512, 2, true>("inverse-like16 9->1 rev", in, out, N, B, 8);
+  run2<9, 1, 1024, 1, true>("inverse-like16 9->1 rev", in, out, N, B, 8);
+  run2<9, 1, 1024, 2, true>("inverse-like16 9->1 rev", in, out, N, B, 4);
+  run2<9, 1, 256, 4, true>("inverse-like16 9->1 rev", in, out, N, B, 2);
+  run2<1, 1, 1024, 2, false>("copy16 1->1", in, out, N, B * 4, 8);
+  run2<9, 0, 512, 2, true>("read-only16 9 rows rev", in, out, N, B, 8);
   return 0;
 }
