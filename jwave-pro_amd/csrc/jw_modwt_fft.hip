@@ -550,6 +550,70 @@ struct InvIn2 {  // item = signal; Z: Q column-major spectra per signal
   }
 };
 
+// ---------------------------------------------------------------------------------------
+// Other lengths N, the fast option: the same pyramid over a power-of-two length P >= N + H
+// (H = (L - 1)(2^J - 1), the longest cumulative filter minus one) instead of a chirp-z
+// transform per DFT.  Every row is a circular convolution of length N with a filter of at most
+// H + 1 taps, so with x_ext[i] = x[(i - H) mod N] (i < N + H; 0 up to P)
+//   (x (*)_N f)[t] = (x_ext (*)_P f)[t + H],   t < N
+// -- no index of the window wraps modulo P -- and the adjoint (correlation) likewise reads
+// c_ext[i] = c[i mod N] (i < N + H) and keeps t < N.  F_P(k), the filters' P-point responses,
+// are the power-of-two pair tables of length P.  One P-point FFT per transform instead of two
+// M-point ones (M >= 2N), the same values up to rounding.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ long wrap_index(long i, long N) {
+  if (i >= N) {
+    i -= N;
+  } else if (i < 0) {
+    i += N;
+  }
+  if (i < 0 || i >= N) i = ((i % N) + N) % N;  // filters longer than the signal
+  return i;
+}
+struct RealInExt {  // x_ext[k] = x[(k - H) mod N] (k < N + H), element k = N2 k1 + col
+  static constexpr bool kStrided = true;
+  const double* x;
+  long N, N2, H;
+  __device__ cplx operator()(long item, long k1, long col) const {
+    const long k = N2 * k1 + col;
+    return make_double2(k < N + H ? x[item * N + wrap_index(k - H, N)] : 0.0, 0.0);
+  }
+};
+struct RealOut2Ext {  // window [H, H + N) of the P-point rows 2q, 2q + 1
+  double* out;
+  long N, N1, H;
+  int J, Q;
+  double inv_p;
+  __device__ void operator()(long item, long idx, long line, cplx v) const {
+    const long sig = item / Q, q = item - sig * Q, t = line + N1 * idx - H;
+    if (t < 0 || t >= N) return;
+    double* o = out + (sig * (J + 1) + 2 * q) * N + t;
+    o[0] = v.x * inv_p;
+    if (2 * q + 1 <= J) o[N] = v.y * inv_p;
+  }
+};
+struct RealIn2Ext {  // rows 2q + i 2q+1 extended: c_ext[k] = c[k mod N] (k < N + H)
+  static constexpr bool kStrided = true;
+  const double* x;
+  long N, N2, H;
+  int J, Q;
+  __device__ cplx operator()(long item, long k1, long col) const {
+    const long sig = item / Q, q = item - sig * Q, k = N2 * k1 + col;
+    if (k >= N + H) return make_double2(0.0, 0.0);
+    const double* r = x + (sig * (J + 1) + 2 * q) * N + wrap_index(k, N);
+    return make_double2(r[0], 2 * q + 1 <= J ? r[N] : 0.0);
+  }
+};
+struct RealOutExt {  // window [0, N) of the P-point row
+  double* out;
+  long N, N1;
+  double inv_p;
+  __device__ void operator()(long item, long idx, long line, cplx v) const {
+    const long t = line + N1 * idx;
+    if (t < N) out[item * N + t] = v.x * inv_p;
+  }
+};
+
 // filter products F ((J+1) rows, scratch) -> pair tables P (2Q rows), spectra layout.
 // P depends on the filters, N and J alone, so it is built once per (device, filters, N, J)
 // and kept, like the twiddle and chirp-z tables: the first call for a key synchronises its
@@ -601,62 +665,95 @@ long chunk_pairs(long N, int J, int batch) {
 }
 }  // namespace
 
+namespace {
+// history of the deepest cumulative filter (the padded path's H)
+long pyramid_hist(const ModwtPlan& p, int J) { return (long)(p.L - 1) * ((1L << J) - 1); }
+// the padded path's length for a length N that is not a power of two (0: use the chirp-z one)
+long padded_len(const ModwtPlan& p, long N, int J) {
+  const long need = N + pyramid_hist(p, J);
+  long P = 1;
+  while (P < need) P <<= 1;
+  return P <= (1L << 23) ? P : 0;
+}
+}  // namespace
+
 int modwt_forward_fft_device(const ModwtPlan& p, const double* x, double* coeffs, long N, int J,
                              int batch, hipStream_t s) {
-  if (!is_pow2(N)) return forward_any(p, x, coeffs, N, J, batch, s);
+  const long P = is_pow2(N) ? N : padded_len(p, N, J);
+  if (P == 0) return forward_any(p, x, coeffs, N, J, batch, s);
+  const long H = P == N ? 0 : pyramid_hist(p, J);
   StreamAllocs mem(s);
   Tables T;
-  int st = fft::tables(N, &T);
+  int st = fft::tables(P, &T);
   if (st != JW_OK) return st;
   // forward FFTs read natural-order rows (split N1n), the inverse FFTs column-major spectra
   // (split N1 x N2, the spectra's layout)
-  const long N1n = fft::split_n1(N, true), N1 = fft::split_n1(N, false), N2 = N / N1;
+  const long N1n = fft::split_n1(P, true), N1 = fft::split_n1(P, false), N2 = P / N1;
   const int Q = (J + 2) / 2;
-  cplx* P = nullptr;
-  st = pair_tables(p, N, J, N1, N2, T, &P, mem, s);
+  cplx* PT = nullptr;
+  st = pair_tables(p, P, J, N1, N2, T, &PT, mem, s);
   if (st != JW_OK) return st;
-  const long bc = chunk_pairs(N, J, batch);
+  const long bc = chunk_pairs(P, J, batch);
   cplx *X = nullptr, *A = nullptr;
-  JW_HIP_TRY(mem.alloc(&X, (size_t)bc * N * sizeof(cplx)));
-  JW_HIP_TRY(mem.alloc(&A, (size_t)bc * Q * N * sizeof(cplx)));
+  JW_HIP_TRY(mem.alloc(&X, (size_t)bc * P * sizeof(cplx)));
+  JW_HIP_TRY(mem.alloc(&A, (size_t)bc * Q * P * sizeof(cplx)));
+  const double inv = 1.0 / (double)P;
   for (long b0 = 0; b0 < batch && st == JW_OK; b0 += bc) {
     const long nb = std::min<long>(bc, batch - b0);
-    st = fft::run_fft<-1>(N, nb, RealIn{x + b0 * N, N, N / N1n}, fft::SpecOut1{X, N, 0},
-                          fft::SpecOut{X, N, N1n, N1, N2, 0}, A, s, T, false);
-    if (st != JW_OK) break;
-    const double inv = 1.0 / (double)N;
     double* o = coeffs + b0 * (long)(J + 1) * N;
-    st = fft::run_fft<1>(N, nb * Q, FwdIn2{X, P, N, N1, N2, Q}, RealOut2{o, N, 1, J, Q, inv},
-                         RealOut2{o, N, N1, J, Q, inv}, A, s, T, false);
+    if (H == 0) {
+      st = fft::run_fft<-1>(P, nb, RealIn{x + b0 * N, N, P / N1n}, fft::SpecOut1{X, P, 0},
+                            fft::SpecOut{X, P, N1n, N1, N2, 0}, A, s, T, false);
+      if (st != JW_OK) break;
+      st = fft::run_fft<1>(P, nb * Q, FwdIn2{X, PT, P, N1, N2, Q}, RealOut2{o, N, 1, J, Q, inv},
+                           RealOut2{o, N, N1, J, Q, inv}, A, s, T, false);
+    } else {
+      st = fft::run_fft<-1>(P, nb, RealInExt{x + b0 * N, N, P / N1n, H}, fft::SpecOut1{X, P, 0},
+                            fft::SpecOut{X, P, N1n, N1, N2, 0}, A, s, T, false);
+      if (st != JW_OK) break;
+      st = fft::run_fft<1>(P, nb * Q, FwdIn2{X, PT, P, N1, N2, Q},
+                           RealOut2Ext{o, N, 1, H, J, Q, inv}, RealOut2Ext{o, N, N1, H, J, Q, inv},
+                           A, s, T, false);
+    }
   }
   return st;
 }
 
 int modwt_inverse_fft_device(const ModwtPlan& p, const double* coeffs, double* x, long N, int J,
                              int batch, hipStream_t s) {
-  if (!is_pow2(N)) return inverse_any(p, coeffs, x, N, J, batch, s);
+  const long P = is_pow2(N) ? N : padded_len(p, N, J);
+  if (P == 0) return inverse_any(p, coeffs, x, N, J, batch, s);
+  const long H = P == N ? 0 : pyramid_hist(p, J);
   StreamAllocs mem(s);
   Tables T;
-  int st = fft::tables(N, &T);
+  int st = fft::tables(P, &T);
   if (st != JW_OK) return st;
-  const long N1n = fft::split_n1(N, true), N1 = fft::split_n1(N, false), N2 = N / N1;
+  const long N1n = fft::split_n1(P, true), N1 = fft::split_n1(P, false), N2 = P / N1;
   const int Q = (J + 2) / 2;
-  cplx* P = nullptr;
-  st = pair_tables(p, N, J, N1, N2, T, &P, mem, s);
+  cplx* PT = nullptr;
+  st = pair_tables(p, P, J, N1, N2, T, &PT, mem, s);
   if (st != JW_OK) return st;
-  const long bc = chunk_pairs(N, J, batch);
+  const long bc = chunk_pairs(P, J, batch);
   cplx *Z = nullptr, *A = nullptr;
-  JW_HIP_TRY(mem.alloc(&Z, (size_t)bc * Q * N * sizeof(cplx)));
-  JW_HIP_TRY(mem.alloc(&A, (size_t)bc * Q * N * sizeof(cplx)));
+  JW_HIP_TRY(mem.alloc(&Z, (size_t)bc * Q * P * sizeof(cplx)));
+  JW_HIP_TRY(mem.alloc(&A, (size_t)bc * Q * P * sizeof(cplx)));
+  const double inv = 1.0 / (double)P;
   for (long b0 = 0; b0 < batch && st == JW_OK; b0 += bc) {
     const long nb = std::min<long>(bc, batch - b0);
-    st = fft::run_fft<-1>(N, nb * Q, RealIn2{coeffs + b0 * (long)(J + 1) * N, N, N / N1n, J, Q},
-                          fft::SpecOut1{Z, N, 0}, fft::SpecOut{Z, N, N1n, N1, N2, 0}, A, s, T,
-                          false);
-    if (st != JW_OK) break;
-    const double inv = 1.0 / (double)N;
-    st = fft::run_fft<1>(N, nb, InvIn2{Z, P, N, N1, N2, Q}, RealOut{x + b0 * N, N, 1, inv},
-                         RealOut{x + b0 * N, N, N1, inv}, A, s, T, false);
+    const double* c = coeffs + b0 * (long)(J + 1) * N;
+    if (H == 0) {
+      st = fft::run_fft<-1>(P, nb * Q, RealIn2{c, N, P / N1n, J, Q}, fft::SpecOut1{Z, P, 0},
+                            fft::SpecOut{Z, P, N1n, N1, N2, 0}, A, s, T, false);
+      if (st != JW_OK) break;
+      st = fft::run_fft<1>(P, nb, InvIn2{Z, PT, P, N1, N2, Q}, RealOut{x + b0 * N, N, 1, inv},
+                           RealOut{x + b0 * N, N, N1, inv}, A, s, T, false);
+    } else {
+      st = fft::run_fft<-1>(P, nb * Q, RealIn2Ext{c, N, P / N1n, H, J, Q}, fft::SpecOut1{Z, P, 0},
+                            fft::SpecOut{Z, P, N1n, N1, N2, 0}, A, s, T, false);
+      if (st != JW_OK) break;
+      st = fft::run_fft<1>(P, nb, InvIn2{Z, PT, P, N1, N2, Q}, RealOutExt{x + b0 * N, N, 1, inv},
+                           RealOutExt{x + b0 * N, N, N1, inv}, A, s, T, false);
+    }
   }
   return st;
 }
