@@ -199,11 +199,18 @@ struct ScaleIn {  // X[sig][k] * conj(psi_hat(omega_k, a_s)), k = N2 k1 + col; i
   PairMap pm;
   double fs;
   const double* sc;  // per scale (MORLET, MEXHAT): {bin step, norm * sqrt(a)}, see cwt_fft_device
+  const double* band;  // per scale (MORLET, MEXHAT): signed bins {lo, hi} of the e^-60 band
   __device__ cplx operator()(long item, long k1, long col) const {
     long sig;
     int s;
     pm.split(pair0 + item, sig, s);
     const long k = N2 * k1 + col;
+    if constexpr (K == JW_CWT_MORLET || K == JW_CWT_MEXHAT) {
+      // bins where psi_hat is below e^-60 of its peak (cwt_band, the band kernel's cut): zero,
+      // without the exp or the X read
+      const double kk = (double)(k > N / 2 ? k - N : k);
+      if (kk < band[2 * s] || kk > band[2 * s + 1]) return make_double2(0.0, 0.0);
+    }
     const cplx wv = psi_bin<K>(w, scales, sc, s, k, N, fs);
     if (wv.x == 0.0 && wv.y == 0.0) return make_double2(0.0, 0.0);  // skip the X read
     const cplx xv = X[sig * N + col * N1 + k1];
@@ -443,7 +450,7 @@ __global__ __launch_bounds__(512) void cwt_band512(const cplx* __restrict__ Xn,
 // f = kk a fs / N; Mexican hat: u = sigma^2 om^2 / 2 with u - ln u <= E + 1 (om^2 e^-u
 // against its peak 2/(e sigma^2)), om = 2 pi kk a fs / N.  Two bins of margin each side.
 static bool cwt_band(int wavelet, const WaveletFT& w, double a, double fs, long N, long* b0,
-                     int* nb) {
+                     int* nb, double* lo_out = nullptr, double* hi_out = nullptr) {
   double lo, hi;
   if (wavelet == JW_CWT_MORLET) {
     const double step = a * fs / (double)N;
@@ -462,6 +469,8 @@ static bool cwt_band(int wavelet, const WaveletFT& w, double a, double fs, long 
     return false;
   }
   if (!(lo > -(double)(N / 2)) || !(hi < (double)(N / 2))) return false;
+  if (lo_out) *lo_out = lo;
+  if (hi_out) *hi_out = hi;
   const long blo = (long)std::floor(lo / 512.0), bhi = (long)std::floor(hi / 512.0);
   const long N1 = N / 512;
   *nb = (int)(bhi - blo + 1);
@@ -552,13 +561,23 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   const long a_items = std::max(gsig, pipe ? 2 * gpair : gpair);
   JW_HIP_TRY(mem.alloc(&X, (size_t)batch * N * sizeof(cplx)));
   JW_HIP_TRY(mem.alloc(&A, (size_t)a_items * N * sizeof(cplx)));
-  // device scale table: [a_0 .. a_{ns-1} | (step, norm*sqrt(a)) per scale] (ScaleIn)
-  std::vector<double> hsc(3 * (size_t)ns);
+  // device scale table: [a_0 .. a_{ns-1} | (step, norm*sqrt(a)) per scale | (lo, hi) per scale]
+  // (ScaleIn); (lo, hi) = the e^-60 band in signed bins, or the whole spectrum
+  std::vector<double> hsc(5 * (size_t)ns);
   for (int i = 0; i < ns; ++i) {
     const double a = scales_host[i];
     hsc[i] = a;
     hsc[ns + 2 * i] = wavelet == JW_CWT_MEXHAT ? 2.0 * kPi * a * fs / (double)N : a * fs / (double)N;
     hsc[ns + 2 * i + 1] = w.norm * std::sqrt(a);
+    long b0;
+    int nb;
+    double lo = -(double)N, hi = (double)N;
+    if (!cwt_band(wavelet, w, a, fs, N, &b0, &nb, &lo, &hi)) {
+      lo = -(double)N;
+      hi = (double)N;
+    }
+    hsc[3 * ns + 2 * i] = lo;
+    hsc[3 * ns + 2 * i + 1] = hi;
   }
   JW_HIP_TRY(mem.alloc(&dsc, hsc.size() * sizeof(double)));
   JW_HIP_TRY(upload_async(dsc, hsc.data(), hsc.size() * sizeof(double), s));
@@ -626,7 +645,7 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     auto go = [&](auto kind) {
       constexpr int K = decltype(kind)::value;
       auto mk_in = [&](long p0) {
-        return ScaleIn<K>{X, dsc, w, N, N1, N / N1, p0, pmf, fs, dsc + ns};
+        return ScaleIn<K>{X, dsc, w, N, N1, N / N1, p0, pmf, fs, dsc + ns, dsc + 3 * ns};
       };
       auto mk_out = [&](long p0) {
         return CoefOut{out, n, N1, p0, 1.0 / (double)N, (ntm & 2) != 0, pmf};
@@ -648,7 +667,7 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     CoefOut o1{out, n, 1, p0, 1.0 / (double)N, (ntm & 2) != 0, pmf};
     auto go = [&](auto kind) {
       ScaleIn<decltype(kind)::value> in{X, dsc, w, N, N1, N <= 4096 ? 1 : N / N1, p0, pmf, fs,
-                                        dsc + ns};
+                                        dsc + ns, dsc + 3 * ns};
       return run_fft<1>(N, np_, in, o1, o, A, s, T, (ntm & 1) != 0);
     };
     switch (wavelet) {

@@ -108,6 +108,44 @@ __device__ __forceinline__ void fft512_wave(cplx (&a)[8], cplx* xb, const cplx* 
   dft8<S>(a);
 }
 
+// The same transform with the two transposes through a buffer of doubles (576 per wave, half
+// the bytes): real parts first, then imaginary parts, through the same conflict-free index
+// maps.  Twice the LDS instructions, half the LDS footprint: the 512-point passes that use it
+// fit three workgroups per CU instead of two.
+template <int S, class WF, class RF>
+__device__ __forceinline__ void exchange_split(cplx (&a)[8], double* xb, WF widx, RF ridx) {
+  double t[8];
+  wave_sync();
+#pragma unroll
+  for (int q = 0; q < 8; ++q) xb[widx(q)] = a[q].x;
+  wave_sync();
+#pragma unroll
+  for (int q = 0; q < 8; ++q) t[q] = xb[ridx(q)];
+  wave_sync();
+#pragma unroll
+  for (int q = 0; q < 8; ++q) xb[widx(q)] = a[q].y;
+  wave_sync();
+#pragma unroll
+  for (int q = 0; q < 8; ++q) a[q] = make_double2(t[q], xb[ridx(q)]);
+}
+
+template <int S>
+__device__ __forceinline__ void fft512_wave_split(cplx (&a)[8], double* xb,
+                                                  const cplx* __restrict__ tw, int lane) {
+  dft8<S>(a);
+#pragma unroll
+  for (int q = 1; q < 8; ++q) a[q] = cmul_tw<S>(a[q], tw[lane * q]);
+  const int q8 = lane >> 3, l1 = lane & 7;
+  exchange_split<S>(a, xb, [&](int q) { return q * 72 + lane; },
+                    [&](int l2) { return q8 * 72 + l1 + 8 * l2; });
+  dft8<S>(a);
+#pragma unroll
+  for (int k1 = 1; k1 < 8; ++k1) a[k1] = cmul_tw<S>(a[k1], tw[8 * l1 * k1]);
+  exchange_split<S>(a, xb, [&](int k1) { return q8 * 72 + l1 * 9 + k1; },
+                    [&](int m) { return q8 * 72 + m * 9 + l1; });
+  dft8<S>(a);
+}
+
 // Device twiddle tables for a length-N transform (cached per N for the library's lifetime):
 //   w512[j] = e^{2 pi i j/512}           (j < 512)      -- the wave engine's table
 //   lo[j]   = e^{2 pi i j/N}             (j < Q)        -- Q = 2^ceil(log2 N / 2)

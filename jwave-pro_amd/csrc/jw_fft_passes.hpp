@@ -35,9 +35,84 @@ static_assert(kTile >= kT * fft::kXbuf, "tile must hold the exchange buffers");
 // lanes of every write group on one bank group (SQ_LDS_BANK_CONFLICT = 62 % of LDS cycles).
 __device__ __forceinline__ int out_slot(int n, int c) { return 8 * n + (c ^ ((n >> 3) & 7)); }
 
+constexpr int kTileD = kT * fft::kXbuf;  // doubles: the split passes' tile (36.9 KB)
+static_assert(kTileD >= kT * 512, "split tile must hold the 8-line staging");
+
 template <int S, bool TWID, class Out>
 __device__ __forceinline__ void pass512_tail(cplx (&a)[8], const Out& out, long N, long N2,
                                              const Tables& T, long item, long line0, cplx* tile);
+
+// The four-step twiddle W_N^(S n1 col) of pass 1 on wave c's outputs n1 = q + 8 k1 + 64 k2.
+__device__ __forceinline__ void twiddle_cols(cplx (&a)[8], int S, long N, const Tables& T,
+                                             long col, int q, int k1) {
+  // one table lookup per lane, then the wave-uniform step W_N^(64 col) applied k2 times
+  // (7 products: ~1e-15 relative)
+  cplx w = fft::twiddle(T, ((long)(q + 8 * k1) * col) & (N - 1));
+  const cplx step = fft::twiddle(T, (64 * col) & (N - 1));
+#pragma unroll
+  for (int k2 = 0; k2 < 8; ++k2) {
+    a[k2] = S < 0 ? fft::cmul_tw<-1>(a[k2], w) : fft::cmul_tw<1>(a[k2], w);
+    if (k2 < 7) w = fft::cmul(w, step);
+  }
+}
+
+// pass512_tail with the re/im-split buffers (tile: kTileD doubles): same values, same output
+// order, half the LDS.
+template <int S, bool TWID, class Out>
+__device__ __forceinline__ void pass512_tail_split(cplx (&a)[8], const Out& out, long N, long N2,
+                                                   const Tables& T, long item, long line0,
+                                                   double* tile) {
+  const int tid = threadIdx.x, lane = tid & 63, c = tid >> 6;
+  fft::fft512_wave_split<S>(a, tile + c * fft::kXbuf, T.w512, lane);
+  const int q = lane >> 3, k1 = lane & 7;
+  if (TWID && N2 > 1) twiddle_cols(a, S, N, T, line0 + c, q, k1);
+  double re[8];
+  __syncthreads();
+#pragma unroll
+  for (int k2 = 0; k2 < 8; ++k2) tile[out_slot(q + 8 * k1 + 64 * k2, c)] = a[k2].x;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) re[i] = tile[out_slot((tid >> 3) + 64 * i, tid & 7)];
+  __syncthreads();
+#pragma unroll
+  for (int k2 = 0; k2 < 8; ++k2) tile[out_slot(q + 8 * k1 + 64 * k2, c)] = a[k2].y;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int n = (tid >> 3) + 64 * i, cc = tid & 7;
+    out(item, n, line0 + cc, make_double2(re[i], tile[out_slot(n, cc)]));
+  }
+}
+
+template <int S, bool IN_TILE, bool TWID, class In, class Out>
+__device__ __forceinline__ void pass512_body_split(const In& in, const Out& out, long N, long N2,
+                                                   const Tables& T, long item, long line0,
+                                                   double* tile) {
+  const int tid = threadIdx.x, lane = tid & 63, c = tid >> 6;
+  cplx a[8];
+  if (IN_TILE) {
+    // tile[k1][c] <- in(k1, line0 + c): 8 consecutive columns per row, coalesced
+    cplx v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = in(item, (tid >> 3) + 64 * i, line0 + (tid & 7));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) tile[((tid >> 3) + 64 * i) * (kT + 1) + (tid & 7)] = v[i].x;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) a[r].x = tile[(lane + 64 * r) * (kT + 1) + c];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) tile[((tid >> 3) + 64 * i) * (kT + 1) + (tid & 7)] = v[i].y;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) a[r].y = tile[(lane + 64 * r) * (kT + 1) + c];
+    __syncthreads();
+  } else {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) a[r] = in(item, lane + 64 * r, line0 + c);
+  }
+  pass512_tail_split<S, TWID>(a, out, N, N2, T, item, line0, tile);
+}
 
 // IN_TILE: the line's inputs are strided (pass 1 over a natural-order array): stage 8 lines
 // through the tile.  TWID: apply the four-step twiddle W_N^(S n1 col) (pass 1).
@@ -98,8 +173,8 @@ __device__ __forceinline__ void pass512_tail(cplx (&a)[8], const Out& out, long 
 
 template <int S, bool IN_TILE, bool TWID, class In, class Out>
 __global__ __launch_bounds__(512) void pass512(In in, Out out, long N, long N2, Tables T) {
-  __shared__ cplx tile[kTile];
-  pass512_body<S, IN_TILE, TWID>(in, out, N, N2, T, blockIdx.y, (long)blockIdx.x * kT, tile);
+  __shared__ double tile[kTileD];
+  pass512_body_split<S, IN_TILE, TWID>(in, out, N, N2, T, blockIdx.y, (long)blockIdx.x * kT, tile);
 }
 
 // Two independent 512-line passes in one grid, for software pipelining of a batch of
@@ -128,14 +203,14 @@ struct TwoRoles {
 template <int S, class In0, class Out0, bool IT1, class In1, class Out1>
 __global__ __launch_bounds__(512) void pass512_two(In0 in0, Out0 out0, In1 in1, Out1 out1, long N,
                                                    long N2, TwoRoles R, Tables T) {
-  __shared__ cplx tile[kTile];
+  __shared__ double tile[kTileD];
   int role;
   long item, line0;
   R.pick(blockIdx.x, role, item, line0);
   if (role == 0) {
-    pass512_body<S, false, false>(in0, out0, N, N2, T, item, line0, tile);
+    pass512_body_split<S, false, false>(in0, out0, N, N2, T, item, line0, tile);
   } else {
-    pass512_body<S, IT1, true>(in1, out1, N, N2, T, item, line0, tile);
+    pass512_body_split<S, IT1, true>(in1, out1, N, N2, T, item, line0, tile);
   }
 }
 
