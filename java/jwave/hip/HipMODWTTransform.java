@@ -13,8 +13,11 @@ import jwave.transforms.wavelets.Wavelet;
  * {@code new Transform(new HipMODWTTransform(w))}; the flattened forward/reverse API (:388-443,
  * :853-912) calls these overrides, so it needs no glue of its own.
  *
- * <p>DIRECT results are bit-identical to the JVM's with ARITH_STRICT (the default). AUTO keeps
- * the reference's int32 rule (N * M_j > fftConvolutionThreshold takes the FFT path, :653).
+ * <p>With ARITH_STRICT (the default) every method is bit-identical to the JVM's: DIRECT, and
+ * AUTO / FFT, which decide per level with the reference's int32 rule (N * M_j >
+ * fftConvolutionThreshold takes the FFT path, :653) and run the reference's own FFT convolution
+ * on the FFT levels (radix-2 with recurrence twiddles, Bluestein for other lengths, :752-837).
+ * ARITH_FMA is the fast contract: AUTO runs DIRECT, FFT an exact-twiddle pyramid.
  * The plan (normalised filters, :452-484 and :599-606) is immutable and shared by all threads;
  * {@link #clearFilterCache()} retires it once no call holds it.
  */
