@@ -144,15 +144,19 @@ __device__ __forceinline__ int own_pos(int tl, int k) {
 }
 
 // Workgroup -> (column tile, item).  When the tiles split evenly over the 8 XCDs, every XCD
-// takes its own tiles and runs all items of a tile back to back, so the tile's pass-2
-// twiddles and filter-spectrum columns stay in that XCD's L2.
+// takes its own contiguous eighth of the tiles, and consecutive workgroups of an XCD take
+// ADJACENT tiles of one item: a tile's column pieces are 64 bytes (4 columns of 16 B, 32 B for
+// real input), so the neighbouring tile uses the other half of every 128-byte line while it is
+// in L2.  (Running all items of one tile back to back instead keeps the tile's twiddles and
+// filter-spectrum columns hot, but fetches each data line twice: db4 J=8 AUTO 1,117 vs 1,250
+// Msamples/s, sym8 J=6 1,480 vs 1,645, profiles/r03/ab_tile*.)
 __device__ __forceinline__ void tile_item(int ntiles, long nitems, int* tile, long* item) {
   const long b = (long)blockIdx.x + (long)blockIdx.y * gridDim.x;
   if ((ntiles & 7) == 0) {
-    const int xcd = (int)(b & 7);
+    const int xcd = (int)(b & 7), per = ntiles >> 3;
     const long q = b >> 3;
-    *item = q % nitems;
-    *tile = xcd * (ntiles >> 3) + (int)(q / nitems);
+    *tile = xcd * per + (int)(q % per);
+    *item = q / per;
   } else {
     *tile = (int)(b % ntiles);
     *item = b / ntiles;
