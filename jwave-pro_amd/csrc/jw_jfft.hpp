@@ -147,16 +147,22 @@ __device__ __forceinline__ int own_pos(int tl, int k) {
 // takes its own contiguous eighth of the tiles, and consecutive workgroups of an XCD take
 // ADJACENT tiles of one item: a tile's column pieces are 64 bytes (4 columns of 16 B, 32 B for
 // real input), so the neighbouring tile uses the other half of every 128-byte line while it is
-// in L2.  (Running all items of one tile back to back instead keeps the tile's twiddles and
-// filter-spectrum columns hot, but fetches each data line twice: db4 J=8 AUTO 1,117 vs 1,250
-// Msamples/s, sym8 J=6 1,480 vs 1,645, profiles/r03/ab_tile*.)
+// in L2; items go in pairs per tile, so the tile's twiddles and filter-spectrum columns serve
+// two items per fetch.  (Running all items of one tile back to back instead keeps those hot,
+// but fetches each data line twice: db4 J=8 AUTO 1,117 vs 1,295 Msamples/s, sym8 J=6 1,480 vs
+// 1,695; items one at a time 1,258 / 1,652, in fours 1,258 / 1,653: profiles/r03/ab_tile*.)
 __device__ __forceinline__ void tile_item(int ntiles, long nitems, int* tile, long* item) {
   const long b = (long)blockIdx.x + (long)blockIdx.y * gridDim.x;
   if ((ntiles & 7) == 0) {
     const int xcd = (int)(b & 7), per = ntiles >> 3;
     const long q = b >> 3;
-    *tile = xcd * per + (int)(q % per);
-    *item = q / per;
+    if ((nitems & 1) == 0) {
+      *tile = xcd * per + (int)((q >> 1) % per);
+      *item = (q >> 1) / per * 2 + (q & 1);
+    } else {
+      *tile = xcd * per + (int)(q % per);
+      *item = q / per;
+    }
   } else {
     *tile = (int)(b % ntiles);
     *item = b / ntiles;
