@@ -683,9 +683,9 @@ def main():
             "recon_error_note": ("max_recon_error = max |x - inverse(forward(x))| over every sample "
                                  "of the step (absolute; inputs uniform in [-1, 1)); recon_rms = "
                                  "its root mean square. The STRICT contract reproduces JWave's "
-                                 "DIRECT forward and inverse bit for bit (other_arith."
-                                 "spot_check_vs_oracle), so JWave's own reconstruction at this "
-                                 "configuration has the same error class"),
+                                 "DIRECT forward (other_arith.spot_check_vs_oracle) and inverse "
+                                 "(tests/test_modwt_gpu.py) bit for bit, so JWave's own "
+                                 "reconstruction at this configuration has the same error class"),
             "spot_check_vs_oracle": check,
             "roofline": {
                 "bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
