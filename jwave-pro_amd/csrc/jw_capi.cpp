@@ -218,12 +218,23 @@ size_t pin_doubles() {
   return v;
 }
 
+// bounce buffers per direction: a ring of pin_ring() (JW_PIN_RING for A/B runs, 2..4)
+constexpr int kMaxRing = 4;
+int pin_ring() {
+  static const int v = [] {
+    const char* e = std::getenv("JW_PIN_RING");
+    const int r = e ? std::atoi(e) : 3;
+    return std::max(2, std::min(kMaxRing, r));
+  }();
+  return v;
+}
+
 struct HostStage {
   int dev = -1;
   hipStream_t own = nullptr, h2d = nullptr, d2h = nullptr;
-  double* pin_in[2] = {nullptr, nullptr};
-  double* pin_out[2] = {nullptr, nullptr};
-  hipEvent_t ev_in[2] = {}, ev_out[2] = {};           // bounce buffer reuse
+  double* pin_in[kMaxRing] = {};
+  double* pin_out[kMaxRing] = {};
+  hipEvent_t ev_in[kMaxRing] = {}, ev_out[kMaxRing] = {};  // bounce buffer reuse
   hipEvent_t loaded[2] = {}, done[2] = {}, drained[2] = {};  // sub-batch pipeline
 
   ~HostStage() {
@@ -231,12 +242,15 @@ struct HostStage {
     (void)hipSetDevice(dev);
     for (hipStream_t s : {own, h2d, d2h})
       if (s) (void)hipStreamSynchronize(s);
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kMaxRing; ++i) {
       if (pin_in[i]) (void)hipHostFree(pin_in[i]);
       if (pin_out[i]) (void)hipHostFree(pin_out[i]);
-      for (hipEvent_t e : {ev_in[i], ev_out[i], loaded[i], done[i], drained[i]})
+      for (hipEvent_t e : {ev_in[i], ev_out[i]})
         if (e) (void)hipEventDestroy(e);
     }
+    for (int i = 0; i < 2; ++i)
+      for (hipEvent_t e : {loaded[i], done[i], drained[i]})
+        if (e) (void)hipEventDestroy(e);
     for (hipStream_t s : {own, h2d, d2h})
       if (s) (void)hipStreamDestroy(s);
   }
@@ -245,23 +259,27 @@ struct HostStage {
     dev = device;
     for (hipStream_t* s : {&own, &h2d, &d2h})
       JW_HIP_TRY(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < pin_ring(); ++i) {
       JW_HIP_TRY(hipHostMalloc((void**)&pin_in[i], pin_doubles() * sizeof(double),
                                hipHostMallocDefault));
       JW_HIP_TRY(hipHostMalloc((void**)&pin_out[i], pin_doubles() * sizeof(double),
                                hipHostMallocDefault));
-      for (hipEvent_t* e : {&ev_in[i], &ev_out[i], &loaded[i], &done[i], &drained[i]})
+      for (hipEvent_t* e : {&ev_in[i], &ev_out[i]})
         JW_HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
+    for (int i = 0; i < 2; ++i)
+      for (hipEvent_t* e : {&loaded[i], &done[i], &drained[i]})
+        JW_HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
     return JW_OK;
   }
 
-  // host -> HBM through the bounce buffers on stream cs; returns when the host buffer may be
+  // host -> HBM through the bounce ring on stream cs; returns when the host buffer may be
   // reused (the last DMAs may still be in flight on cs)
   int put(double* dst, const double* src, size_t n, hipStream_t cs) {
+    const int R = pin_ring();
     for (size_t off = 0, k = 0; off < n; off += pin_doubles(), ++k) {
       const size_t c = std::min(pin_doubles(), n - off);
-      const int b = (int)(k & 1);
+      const int b = (int)(k % R);
       JW_HIP_TRY(hipEventSynchronize(ev_in[b]));  // this buffer's previous DMA has landed
       CopyPool::get().copy(pin_in[b], src + off, c * sizeof(double));
       JW_HIP_TRY(hipMemcpyAsync(dst + off, pin_in[b], c * sizeof(double), hipMemcpyHostToDevice, cs));
@@ -270,26 +288,32 @@ struct HostStage {
     return JW_OK;
   }
 
-  // HBM -> host after the work queued on cs; DMA of chunk k overlaps the host copy of k-1
+  // HBM -> host after the work queued on cs: up to R - 1 chunk DMAs in flight ahead of the
+  // host copy of the oldest one
   int get(double* dst, const double* src, size_t n, hipStream_t cs) {
-    size_t prev_off = 0, prev_c = 0;
-    int prev_b = -1;
-    for (size_t off = 0, k = 0; off < n; off += pin_doubles(), ++k) {
-      const size_t c = std::min(pin_doubles(), n - off);
-      const int b = (int)(k & 1);
+    const int R = pin_ring();
+    const size_t P = pin_doubles();
+    const size_t nch = (n + P - 1) / P;
+    auto drain = [&](size_t k) -> int {  // chunk k's DMA has landed: copy it out
+      const int b = (int)(k % R);
+      const size_t off = k * P, c = std::min(P, n - off);
+      JW_HIP_TRY(hipEventSynchronize(ev_out[b]));
+      CopyPool::get().copy(dst + off, pin_out[b], c * sizeof(double));
+      return JW_OK;
+    };
+    for (size_t k = 0; k < nch; ++k) {
+      if (k >= (size_t)R) {  // buffer k % R is free once chunk k - R has been copied out
+        const int r = drain(k - R);
+        if (r != JW_OK) return r;
+      }
+      const int b = (int)(k % R);
+      const size_t off = k * P, c = std::min(P, n - off);
       JW_HIP_TRY(hipMemcpyAsync(pin_out[b], src + off, c * sizeof(double), hipMemcpyDeviceToHost, cs));
       JW_HIP_TRY(hipEventRecord(ev_out[b], cs));
-      if (prev_b >= 0) {
-        JW_HIP_TRY(hipEventSynchronize(ev_out[prev_b]));
-        CopyPool::get().copy(dst + prev_off, pin_out[prev_b], prev_c * sizeof(double));
-      }
-      prev_off = off;
-      prev_c = c;
-      prev_b = b;
     }
-    if (prev_b >= 0) {
-      JW_HIP_TRY(hipEventSynchronize(ev_out[prev_b]));
-      CopyPool::get().copy(dst + prev_off, pin_out[prev_b], prev_c * sizeof(double));
+    for (size_t k = nch > (size_t)R ? nch - R : 0; k < nch; ++k) {
+      const int r = drain(k);
+      if (r != JW_OK) return r;
     }
     return JW_OK;
   }
