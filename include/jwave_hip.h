@@ -23,8 +23,9 @@
  *   - one private stream-ordered memory pool per device for workspaces (the device's default
  *     pool is never touched); it keeps freed memory for reuse, gives it back when an
  *     allocation would fail, and on jw_release_caches();
- *   - per host thread and device, a non-blocking stream and two 32 MiB pinned bounce buffers
- *     for JW_HOST staging.
+ *   - per host thread and device, three non-blocking streams and a ring of three 32 MiB pinned
+ *     bounce buffers per direction (192 MiB) for JW_HOST staging, freed when the thread exits
+ *     (JW_PIN_RING / JW_PIN_MB / JW_COPY_THREADS tune them).
  */
 #ifndef JWAVE_HIP_H
 #define JWAVE_HIP_H
