@@ -200,6 +200,7 @@ struct ScaleIn {  // X[sig][k] * conj(psi_hat(omega_k, a_s)), k = N2 k1 + col; i
   double fs;
   const double* sc;  // per scale (MORLET, MEXHAT): {bin step, norm * sqrt(a)}, see cwt_fft_device
   const double* band;  // per scale (MORLET, MEXHAT): signed bins {lo, hi} of the e^-60 band
+  bool early;  // A/B runs (JW_CWT_EARLY): X read issued before psi_hat's exp (same values)
   __device__ cplx operator()(long item, long k1, long col) const {
     long sig;
     int s;
@@ -210,6 +211,12 @@ struct ScaleIn {  // X[sig][k] * conj(psi_hat(omega_k, a_s)), k = N2 k1 + col; i
       // without the exp or the X read
       const double kk = (double)(k > N / 2 ? k - N : k);
       if (kk < band[2 * s] || kk > band[2 * s + 1]) return make_double2(0.0, 0.0);
+      if (early) {
+        // inside the band psi_hat never underflows, so the X read does not wait for the exp
+        const cplx xv = X[sig * N + col * N1 + k1];
+        const double wv = psi_bin<K>(w, scales, sc, s, k, N, fs).x;
+        return make_double2(xv.x * wv, xv.y * wv);
+      }
     }
     const cplx wv = psi_bin<K>(w, scales, sc, s, k, N, fs);
     if (wv.x == 0.0 && wv.y == 0.0) return make_double2(0.0, 0.0);  // skip the X read
@@ -222,6 +229,24 @@ struct ScaleIn {  // X[sig][k] * conj(psi_hat(omega_k, a_s)), k = N2 k1 + col; i
     }
   }
 };
+struct CoefRow {  // CoefOut with the output pair resolved: one coefficient row
+  double* row;
+  long n, N1;
+  double inv_n;
+  bool nt;
+  __device__ void operator()(long idx, long line, cplx v) const {
+    const long t = line + N1 * idx;
+    if (t < n) {
+      cplx* o = (cplx*)(row + 2 * t);
+      const cplx r = make_double2(v.x * inv_n, v.y * inv_n);
+      if (nt) {
+        nt_store(o, r);
+      } else {
+        *o = r;
+      }
+    }
+  }
+};
 struct CoefOut {  // out[pair][t] = v / N for t = line + N1 * idx < n  (reverse :207-211)
   double* out;  // interleaved (re, im), B x ns x n
   long n, N1, pair0;
@@ -230,7 +255,7 @@ struct CoefOut {  // out[pair][t] = v / N for t = line + N1 * idx < n  (reverse 
   PairMap pm;  // item -> (signal, scale) of the output
   __device__ void operator()(long item, long idx, long line, cplx v) const {
     const long t = line + N1 * idx;
-    const long pr = pm.out_pair(pair0 + item);  // outside the branch: hoisted per workgroup
+    const long pr = pm.out_pair(pair0 + item);
     if (t < n) {
       cplx* o = (cplx*)(out + 2 * (pr * n + t));
       const cplx r = make_double2(v.x * inv_n, v.y * inv_n);
@@ -240,6 +265,9 @@ struct CoefOut {  // out[pair][t] = v / N for t = line + N1 * idx < n  (reverse 
         *o = r;
       }
     }
+  }
+  __device__ CoefRow bind(long item) const {  // fft::bind_out: the pair looked up once per line
+    return CoefRow{out + 2 * pm.out_pair(pair0 + item) * n, n, N1, inv_n, nt};
   }
 };
 
@@ -293,13 +321,15 @@ __global__ __launch_bounds__(256) void cwt_band_roots(double4* w, long N, long N
 // round-robin dispatch), so the pair's band of X is fetched into one L2, not eight (speed only).
 typedef double d4v __attribute__((ext_vector_type(4)));
 
-template <bool MF>
-__global__ __launch_bounds__(512) void cwt_band512(const cplx* __restrict__ Xn,
-                                                   const double* __restrict__ psi,
-                                                   const BandScale* __restrict__ bands, int nband,
-                                                   const double4* __restrict__ wN1, long N, long N1,
-                                                   long items, CoefOut out, Tables T, int R) {
-  __shared__ cplx tile[fft::kTile];
+// MF: band sums on the matrix cores (else VALU, Gauss form); PF: the next block pair's loads
+// issued before the current pair's MFMAs; WPE: waves per SIMD the registers are fitted to (6 =
+// three workgroups per CU, one row group each; 4 = two, R row groups each).
+template <bool MF, bool PF, int WPE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void cwt_band512(
+    const cplx* __restrict__ Xn, const double* __restrict__ psi,
+    const BandScale* __restrict__ bands, int nband, const double4* __restrict__ wN1, long N,
+    long N1, long items, CoefOut out, Tables T, int R) {
+  __shared__ double tile[fft::kTileD];  // re/im-split staging (36.9 KB)
   // 32-bit index math (the scalar unit runs 64-bit division as a ~100-instruction sequence)
   const unsigned lrpp = (unsigned)__builtin_ctzl(N1 / (fft::kT * R)), local = blockIdx.x >> 3;
   const unsigned slot = local >> lrpp;
@@ -311,8 +341,9 @@ __global__ __launch_bounds__(512) void cwt_band512(const cplx* __restrict__ Xn,
   // R row groups per workgroup, one after the other: the output stores of one group drain
   // while the band sums of the next run
   const int tid = threadIdx.x, lane = tid & 63, c = tid >> 6;
-  for (int it = 0; it < R; ++it) {
+  for (int it = 0; it < (WPE > 4 ? 1 : R); ++it) {  // WPE > 4: one group (registers)
   const long r0 = ((long)rg * R + it) * fft::kT;
+  double im[8];  // this thread's 8 elements of the 8 rows of A: imaginary parts (re: the tile)
   __syncthreads();  // the previous group's staging reads are done with the tile
   // thread (h, kp): columns kp and kp + 256, rows r0 + 4h .. r0 + 4h + 3 (h uniform per wave,
   // so each wave-uniform twiddle feeds two columns)
@@ -375,8 +406,11 @@ __global__ __launch_bounds__(512) void cwt_band512(const cplx* __restrict__ Xn,
     const cplx u = fft::twiddle(T, (256L * (rr + t)) & (N - 1));  // uniform: scalar loads
     const cplx v0 = make_double2(s1[0][t] - s2[0][t], s3[0][t] - s1[0][t] - s2[0][t]);
     const cplx v1 = make_double2(s1[1][t] - s2[1][t], s3[1][t] - s1[1][t] - s2[1][t]);
-    tile[(4 * h + t) * 512 + kp] = fft::cmul(v0, w0);
-    tile[(4 * h + t) * 512 + kp + 256] = fft::cmul(v1, fft::cmul(w0, u));
+    const cplx r0v = fft::cmul(v0, w0), r1v = fft::cmul(v1, fft::cmul(w0, u));
+    tile[(4 * h + t) * 512 + kp] = r0v.x;
+    tile[(4 * h + t) * 512 + kp + 256] = r1v.x;
+    im[t] = r0v.y;
+    im[4 + t] = r1v.y;
     if (t < 3) w0 = fft::cmul(w0, st);
   }
   } else {
@@ -394,25 +428,43 @@ __global__ __launch_bounds__(512) void cwt_band512(const cplx* __restrict__ Xn,
   // each lane loads only the part of Z it feeds (re for kq even, im for kq odd): 8-byte loads
   const double* xs = (const double*)(Xn + (long)sig * N + 64 * c + tr) + zc;
   const double* ps = psi + b.psi_off + 64 * c + tr;
-  for (int j0 = 0; j0 < b.nb; j0 += 2) {
+  // loads of the next block pair are issued before the current pair's MFMAs (the L2 latency of
+  // one pair hides under the other's arithmetic); past the band the index clamps to nb - 1 and
+  // the twiddle row is zeroed
+  auto load = [&](int j0, double (&xv)[4], double (&pv)[4], double& av) {
     const int j = j0 + jo;
     const bool in = j < b.nb;
     const int jj = in ? j : b.nb - 1;
     const unsigned k1 = ((unsigned)b.b0 + jj) & m1;
     const double4 w = wN1[(k1 * ((unsigned)r0 + t)) & m1];
     // A[tr][kq]: Re row: (Re W, -Im W) for (Re Z, Im Z); Im row: (Im W, Re W)
-    double av = im_row ? (zc ? w.x : w.y) : (zc ? -w.y : w.x);
+    av = im_row ? (zc ? w.x : w.y) : (zc ? -w.y : w.x);
     av = in ? av : 0.0;
-    double xv[4], pv[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       xv[q] = xs[2 * (512L * k1 + 16 * q)];
       pv[q] = ps[512 * jj + 16 * q];
     }
+  };
+  double xv[4], pv[4], av;
+  load(0, xv, pv, av);
+  for (int j0 = 0; j0 < b.nb; j0 += 2) {
+    double xn[4], pn[4], an;
+    if (PF) load(j0 + 2, xn, pn, an);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const double bv = xv[q] * pv[q];
       acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[q], 0, 0, 0);
+    }
+    if (PF) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        xv[q] = xn[q];
+        pv[q] = pn[q];
+      }
+      av = an;
+    } else {
+      load(j0 + 2, xv, pv, av);
     }
   }
   // lane: D rows (l >> 4) + 4 r -> Re of rows t0, t0 + 4 (r = 0, 1), Im of them (r = 2, 3);
@@ -425,20 +477,34 @@ __global__ __launch_bounds__(512) void cwt_band512(const cplx* __restrict__ Xn,
     const cplx st = fft::twiddle(T, (16 * n1) & (N - 1));
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const cplx v = make_double2(acc[q][e], acc[q][e + 2]);
-      tile[(t0 + 4 * e) * 512 + col0 + 16 * q] = fft::cmul(v, w0);
+      const cplx v = fft::cmul(make_double2(acc[q][e], acc[q][e + 2]), w0);
+      tile[(t0 + 4 * e) * 512 + (int)col0 + 16 * q] = v.x;  // re now, im after the first read
+      im[4 * e + q] = v.y;
       if (q < 3) w0 = fft::cmul(w0, st);
     }
   }
   }
-  __syncthreads();
+  // rows r0 .. r0 + 7 of A through the tile (re, then im) into wave c's line r0 + c
   cplx a[8];
+  __syncthreads();
 #pragma unroll
-  for (int r = 0; r < 8; ++r) a[r] = tile[c * 512 + lane + 64 * r];
+  for (int r = 0; r < 8; ++r) a[r].x = tile[c * 512 + lane + 64 * r];
+  __syncthreads();
+  if constexpr (!MF) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) tile[(4 * (tid >> 8) + (i & 3)) * 512 + (tid & 255) + 256 * (i >> 2)] = im[i];
+  } else {
+    const int t0 = lane >> 4, col0 = 64 * c + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) tile[(t0 + 4 * (i >> 2)) * 512 + col0 + 16 * (i & 3)] = im[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 8; ++r) a[r].y = tile[c * 512 + lane + 64 * r];
   __syncthreads();
   CoefOut o = out;
   o.pair0 = (long)sig * out.pm.ns + b.s;  // one output pair per workgroup
-  fft::pass512_tail<1, false>(a, o, N, 512L, T, 0L, r0, tile);
+  fft::pass512_tail_split<1, false>(a, o, N, 512L, T, 0L, r0, tile);
   }
 }
 
@@ -551,6 +617,8 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   // N = 2^18 (512 x 512): the pairs' inverse FFTs are software-pipelined over two workspaces
   // (run_fft512_pipelined); env JW_CWT_PIPE=0 runs the groups one after the other (A/B runs).
   const char* gpp = std::getenv("JW_CWT_PIPE");
+  const char* gel = std::getenv("JW_CWT_EARLY");
+  const bool early = !(gel && gel[0] == '0');
   const bool pipe = N == (1L << 18) && pairs > gpair && !(gpp && gpp[0] == '0');
   StreamAllocs mem(s);
   cplx *X = nullptr, *A = nullptr, *Xn = nullptr;
@@ -624,19 +692,33 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     JW_HIP_TRY(hipGetLastError());
     const CoefOut ob{out, n, N1b, 0, 1.0 / (double)N, (ntm & 2) != 0, pm_all};
     const long items = (long)batch * nband;
+    // A/B runs: JW_CWT_BAND_V = 2 x (three workgroups per CU, one row group each, instead of
+    // two with R) + (load prefetch); JW_CWT_BAND_MFMA=0: VALU band sums.  Measured at cfg3
+    // (profiles/r03/cwt_band_v.log): band kernel 15.5 (0) / 15.2 (1) / 14.4 (2) / 14.0 ms (3).
+    const char* gbv = std::getenv("JW_CWT_BAND_V");
+    const int bv = gbv ? std::atoi(gbv) : 3;
     const char* grr = std::getenv("JW_CWT_BAND_R");  // A/B runs: row groups per workgroup
-    int R = grr ? std::atoi(grr) : 8;  // measured: 1 -> 44.6, 4 -> 42.5, 8 -> 41.7 ms at cfg3
+    int R = grr ? std::atoi(grr) : 8;  // two workgroups per CU: 1 -> 44.6, 8 -> 41.7 ms (r02)
+    if (bv >= 2) R = 1;
     while (R > 1 && (N1b / fft::kT) % R) R >>= 1;
     R = std::max(1, std::min<int>(R, (int)(N1b / fft::kT)));
     const long blocks = (items + 7) / 8 * 8 * (N1b / fft::kT / R);
     if (blocks > 0x7fffffffL) return fail(JW_ERR_UNSUPPORTED, "CWT band grid too large");
-    const char* gmf = std::getenv("JW_CWT_BAND_MFMA");  // A/B runs: 0 = VALU band sums
+    const char* gmf = std::getenv("JW_CWT_BAND_MFMA");
+    auto band = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(512), 0, s, Xn, psi, dbands, nband,
+                         wN1, N, N1b, items, ob, T, R);
+    };
     if (gmf && gmf[0] == '0') {
-      hipLaunchKernelGGL(cwt_band512<false>, dim3((unsigned)blocks), dim3(512), 0, s, Xn, psi,
-                         dbands, nband, wN1, N, N1b, items, ob, T, R);
+      band(cwt_band512<false, false, 4>);
+    } else if (bv == 0) {
+      band(cwt_band512<true, false, 4>);
+    } else if (bv == 1) {
+      band(cwt_band512<true, true, 4>);
+    } else if (bv == 2) {
+      band(cwt_band512<true, false, 6>);
     } else {
-      hipLaunchKernelGGL(cwt_band512<true>, dim3((unsigned)blocks), dim3(512), 0, s, Xn, psi,
-                         dbands, nband, wN1, N, N1b, items, ob, T, R);
+      band(cwt_band512<true, true, 6>);
     }
     JW_HIP_TRY(hipGetLastError());
   }
@@ -645,7 +727,7 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     auto go = [&](auto kind) {
       constexpr int K = decltype(kind)::value;
       auto mk_in = [&](long p0) {
-        return ScaleIn<K>{X, dsc, w, N, N1, N / N1, p0, pmf, fs, dsc + ns, dsc + 3 * ns};
+        return ScaleIn<K>{X, dsc, w, N, N1, N / N1, p0, pmf, fs, dsc + ns, dsc + 3 * ns, early};
       };
       auto mk_out = [&](long p0) {
         return CoefOut{out, n, N1, p0, 1.0 / (double)N, (ntm & 2) != 0, pmf};
@@ -667,7 +749,7 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     CoefOut o1{out, n, 1, p0, 1.0 / (double)N, (ntm & 2) != 0, pmf};
     auto go = [&](auto kind) {
       ScaleIn<decltype(kind)::value> in{X, dsc, w, N, N1, N <= 4096 ? 1 : N / N1, p0, pmf, fs,
-                                        dsc + ns, dsc + 3 * ns};
+                                        dsc + ns, dsc + 3 * ns, early};
       return run_fft<1>(N, np_, in, o1, o, A, s, T, (ntm & 1) != 0);
     };
     switch (wavelet) {

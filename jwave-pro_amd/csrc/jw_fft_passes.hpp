@@ -42,6 +42,25 @@ template <int S, bool TWID, class Out>
 __device__ __forceinline__ void pass512_tail(cplx (&a)[8], const Out& out, long N, long N2,
                                              const Tables& T, long item, long line0, cplx* tile);
 
+// An output functor with its item fixed before a line's stores.  A functor whose item -> row
+// mapping reads memory (CoefOut's scale map) provides bind(item): the lookup then happens once,
+// not after every store (the compiler cannot hoist a load past stores that may alias it, and on
+// gfx9 the wait for that load also drains every store issued before it).
+template <class Out>
+struct BoundOut {
+  const Out& out;
+  long item;
+  __device__ void operator()(long idx, long line, cplx v) const { out(item, idx, line, v); }
+};
+template <class Out>
+__device__ __forceinline__ auto bind_out(const Out& out, long item) {
+  if constexpr (requires { out.bind(item); }) {
+    return out.bind(item);
+  } else {
+    return BoundOut<Out>{out, item};
+  }
+}
+
 // The four-step twiddle W_N^(S n1 col) of pass 1 on wave c's outputs n1 = q + 8 k1 + 64 k2.
 __device__ __forceinline__ void twiddle_cols(cplx (&a)[8], int S, long N, const Tables& T,
                                              long col, int q, int k1) {
@@ -77,10 +96,11 @@ __device__ __forceinline__ void pass512_tail_split(cplx (&a)[8], const Out& out,
 #pragma unroll
   for (int k2 = 0; k2 < 8; ++k2) tile[out_slot(q + 8 * k1 + 64 * k2, c)] = a[k2].y;
   __syncthreads();
+  const auto o = bind_out(out, item);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int n = (tid >> 3) + 64 * i, cc = tid & 7;
-    out(item, n, line0 + cc, make_double2(re[i], tile[out_slot(n, cc)]));
+    o(n, line0 + cc, make_double2(re[i], tile[out_slot(n, cc)]));
   }
 }
 
@@ -164,10 +184,11 @@ __device__ __forceinline__ void pass512_tail(cplx (&a)[8], const Out& out, long 
 #pragma unroll
   for (int k2 = 0; k2 < 8; ++k2) tile[out_slot(q + 8 * k1 + 64 * k2, c)] = a[k2];
   __syncthreads();
+  const auto o = bind_out(out, item);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int n = (tid >> 3) + 64 * i, cc = tid & 7;
-    out(item, n, line0 + cc, tile[out_slot(n, cc)]);
+    o(n, line0 + cc, tile[out_slot(n, cc)]);
   }
 }
 

@@ -155,6 +155,27 @@ def test_band_scales_one_pass(kind, n, monkeypatch):
         assert nw(band[i], ex[i]) < 1e-11, (i, nw(band[i], ex[i]))
 
 
+@pytest.mark.parametrize("kind", ["morlet", "mexhat"])
+def test_band_and_pass1_variants_bit_identical(kind, monkeypatch):
+    # The band kernel's schedules (JW_CWT_BAND_V: load prefetch, one or eight row groups per
+    # workgroup at 6 or 4 waves per SIMD) and the two-pass first pass with the X read issued
+    # before or after psi_hat's exp (JW_CWT_EARLY) do the same operations: equal bits, at the
+    # cfg3 length with both one-pass and two-pass scales.
+    n = 1 << 18
+    scales = CWT.generateLogScales(2.0, 1024.0, 10)
+    wv = {"morlet": MorletWavelet(*MORLET6), "mexhat": MexicanHatWavelet(1.5)}[kind]
+    x = orc.fill_uniform(n, 9)
+    ref = None
+    for v, e in [("3", "1"), ("0", "0"), ("2", "1"), ("1", "0")]:
+        monkeypatch.setenv("JW_CWT_BAND_V", v)
+        monkeypatch.setenv("JW_CWT_EARLY", e)
+        got = CWT(wv).transformFFT(x, scales, 1.0).getCoefficients()
+        if ref is None:
+            ref = got
+        else:
+            assert np.array_equal(got, ref), (v, e)
+
+
 def test_result_accessors_on_device(device):
     # CWTResult.getMagnitude / getPhase / getScalogram (CWTResult.java:94-126, :272-287) on
     # device coefficients (jw_cwt_magnitude / _phase / _scalogram): no host copy of the
