@@ -24,14 +24,17 @@ using cplx = double2;
 
 __device__ __forceinline__ cplx cadd(cplx a, cplx b) { return make_double2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ cplx csub(cplx a, cplx b) { return make_double2(a.x - b.x, a.y - b.y); }
-// a * w^S for a table entry w = e^{+i theta} (S = -1 uses the conjugate)
+// a * w^S for a table entry w = e^{+i theta} (S = -1 uses the conjugate).  This engine is the
+// exact-twiddle one (tolerance contract, not the reference's operation order -- that is
+// jw_jfft.hpp), so the complex products use fused multiply-adds: two FP64 instructions fewer per
+// product, and at FP64 every wave64 VALU instruction holds its SIMD four cycles.
 template <int S>
 __device__ __forceinline__ cplx cmul_tw(cplx a, cplx w) {
   const double wy = S > 0 ? w.y : -w.y;
-  return make_double2(a.x * w.x - a.y * wy, a.x * wy + a.y * w.x);
+  return make_double2(__builtin_fma(a.x, w.x, -(a.y * wy)), __builtin_fma(a.x, wy, a.y * w.x));
 }
 __device__ __forceinline__ cplx cmul(cplx a, cplx b) {
-  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+  return make_double2(__builtin_fma(a.x, b.x, -(a.y * b.y)), __builtin_fma(a.x, b.y, a.y * b.x));
 }
 
 // In-register 8-point DFT, v[q] <- sum_r v[r] e^{S 2 pi i r q / 8} (radix-2 DIF, bit-reversed
