@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <memory>
 #include <type_traits>
 #include <vector>
 
@@ -510,6 +511,51 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
 
 }  // namespace
 
+// A second stream per (host thread, device) for the band kernel, so that it runs beside the
+// two-pass pipeline instead of before it: the band kernel is FP64-issue and latency bound
+// (§5.4 of DESIGN.md), the two-pass passes mostly HBM bound, and run together they share the
+// CUs.  fork: the band kernel waits for everything queued on the caller's stream so far; join:
+// the caller's stream waits for the band kernel before anything after it (and before the
+// stream-ordered frees of the call's buffers).
+struct SideStream {
+  int dev = -1;
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  ~SideStream() {
+    if (dev < 0) return;
+    (void)hipSetDevice(dev);
+    if (s) (void)hipStreamSynchronize(s);
+    if (fork) (void)hipEventDestroy(fork);
+    if (join) (void)hipEventDestroy(join);
+    if (s) (void)hipStreamDestroy(s);
+  }
+};
+static int side_stream(SideStream** out) {
+  static thread_local std::vector<std::unique_ptr<SideStream>> sides;  // by device ordinal
+  int dev = 0;
+  JW_HIP_TRY(hipGetDevice(&dev));
+  if ((int)sides.size() <= dev) sides.resize(dev + 1);
+  if (!sides[dev]) {
+    auto ss = std::make_unique<SideStream>();
+    ss->dev = dev;
+    JW_HIP_TRY(hipStreamCreateWithFlags(&ss->s, hipStreamNonBlocking));
+    JW_HIP_TRY(hipEventCreateWithFlags(&ss->fork, hipEventDisableTiming));
+    JW_HIP_TRY(hipEventCreateWithFlags(&ss->join, hipEventDisableTiming));
+    sides[dev] = std::move(ss);
+  }
+  *out = sides[dev].get();
+  return JW_OK;
+}
+// Destroyed before the StreamAllocs declared ahead of it: the caller's stream waits for the side
+// stream's work before the buffers that work reads are freed.
+struct JoinGuard {
+  hipStream_t s = nullptr;
+  SideStream* side = nullptr;
+  ~JoinGuard() {
+    if (side) (void)hipStreamWaitEvent(s, side->join, 0);
+  }
+};
+
 // The band of scale a (bins whose psi_hat is above e^-kBandE of its peak) as 512-bin blocks
 // b0 .. b0 + nb - 1 mod N1; false when the band is not known in closed form (Paul, DOG,
 // Meyer) or wraps the whole spectrum.  Morlet: |f - fc| <= sqrt(E / (2 pi^2 fb)) with
@@ -621,6 +667,7 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   const bool early = !(gel && gel[0] == '0');
   const bool pipe = N == (1L << 18) && pairs > gpair && !(gpp && gpp[0] == '0');
   StreamAllocs mem(s);
+  JoinGuard join{s, nullptr};  // declared after mem: joins before mem's frees
   cplx *X = nullptr, *A = nullptr, *Xn = nullptr;
   double4* wN1 = nullptr;
   double *dsc = nullptr, *psi = nullptr;
@@ -705,8 +752,20 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     const long blocks = (items + 7) / 8 * 8 * (N1b / fft::kT / R);
     if (blocks > 0x7fffffffL) return fail(JW_ERR_UNSUPPORTED, "CWT band grid too large");
     const char* gmf = std::getenv("JW_CWT_BAND_MFMA");
+    // with two-pass pairs to follow, the band kernel runs on the side stream beside them
+    // (env JW_CWT_OVERLAP=0: one after the other, A/B runs)
+    const char* gov = std::getenv("JW_CWT_OVERLAP");
+    hipStream_t bs = s;
+    if (pairs > 0 && !(gov && gov[0] == '0')) {
+      SideStream* side = nullptr;
+      if ((st = side_stream(&side)) != JW_OK) return st;
+      JW_HIP_TRY(hipEventRecord(side->fork, s));
+      JW_HIP_TRY(hipStreamWaitEvent(side->s, side->fork, 0));
+      bs = side->s;
+      join.side = side;  // armed before the launch: any exit below joins
+    }
     auto band = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(512), 0, s, Xn, psi, dbands, nband,
+      hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(512), 0, bs, Xn, psi, dbands, nband,
                          wN1, N, N1b, items, ob, T, R);
     };
     if (gmf && gmf[0] == '0') {
@@ -721,6 +780,7 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
       band(cwt_band512<true, true, 6>);
     }
     JW_HIP_TRY(hipGetLastError());
+    if (join.side) JW_HIP_TRY(hipEventRecord(join.side->join, bs));
   }
   // the other (signal, scale) pairs: IFFT(X * psi_hat) -> coefficients in two passes
   if (pipe && st == JW_OK) {
