@@ -391,11 +391,59 @@ __global__ __launch_bounds__(kNT2) void fwt_rev_lds2(const double* __restrict__ 
 // ---------------------------------------------------------------------------------------
 constexpr int kRowN = 4096;
 constexpr int kRowMaxM = 20;  // longer filters keep the runtime-level kernels (compile time)
+#ifndef JW_REV_PAIRS2
+#define JW_REV_PAIRS2 1
+#endif
+constexpr bool kRevPairs2 = JW_REV_PAIRS2;  // row kernels: two outputs per lane (A/B builds: 0)
 
 template <bool FMA, int M, int H>
 __device__ __forceinline__ void row_fwd_level(double* buf, double* ys, int tid, const Filters& f) {
   constexpr int half = H / 2, P = half >= kNT2 ? half / kNT2 : 1, PAD = M - 2;
   constexpr bool padded = H >= PAD;  // single wrap, read from the copy after the end
+  if constexpr (padded && P >= 2 && kRevPairs2) {
+    // two adjacent outputs (2v, 2v + 1) per lane, v = tid + r kNT2: output i reads
+    // buf[2i .. 2i + M), so the pair shares M - 2 inputs and the lane loads M/2 + 1 aligned
+    // 16-byte pairs instead of M; each sum keeps the one-output order (bit-identical)
+    double lo[P], hi[P];
+#pragma unroll
+    for (int r = 0; r < P / 2; ++r) {
+      const int i0 = 2 * (tid + r * kNT2);
+      double v[M + 2];
+#pragma unroll
+      for (int q = 0; q <= M / 2; ++q) {
+        const d2 w = *(const d2*)&buf[2 * i0 + 2 * q];
+        v[2 * q] = w.x;
+        v[2 * q + 1] = w.y;
+      }
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        double l = 0., h = 0.;
+#pragma unroll
+        for (int t = 0; t < (M >> 1); ++t) {
+          const double x0 = v[2 * e + 2 * t], x1 = v[2 * e + 2 * t + 1];
+          l = madd<FMA>(l, f.sD[2 * t], x0);
+          h = madd<FMA>(h, f.wD[2 * t], x0);
+          l = madd<FMA>(l, f.sD[2 * t + 1], x1);
+          h = madd<FMA>(h, f.wD[2 * t + 1], x1);
+        }
+        lo[2 * r + e] = l;
+        hi[2 * r + e] = h;
+      }
+    }
+    __syncthreads();  // every read of buf[0 .. H + PAD) is done
+#pragma unroll
+    for (int r = 0; r < P / 2; ++r) {
+      const int i0 = 2 * (tid + r * kNT2);
+      *(d2*)&buf[i0] = d2{lo[2 * r], lo[2 * r + 1]};
+      *(d2*)&ys[half + i0] = d2{hi[2 * r], hi[2 * r + 1]};
+    }
+    // the next level's wrap copy (its first PAD inputs are this level's lo[0 .. PAD))
+    if constexpr (PAD > 0 && half >= PAD) {
+      if (2 * tid < PAD) *(d2*)&buf[half + 2 * tid] = d2{lo[0], lo[1]};
+    }
+    __syncthreads();
+    return;
+  }
   double lo[P], hi[P];
 #pragma unroll
   for (int r = 0; r < P; ++r) {
@@ -462,11 +510,94 @@ __global__ __launch_bounds__(kNT2) void fwt_fwd_row(const double* x, double* y, 
   for (int i = tid; i < hcur; i += kNT2) ys[i] = buf[i];
 }
 
+// Two adjacent pairs (u, u + 1) of an unwrapped reverse level from one lane: pair u reads
+// buf[u - t] and buf[u - t + half] for t < M/2, pair u + 1 the same shifted by one, so the lane
+// loads the M/2 + 1 values of each half once, as aligned 16-byte pairs (u even), instead of
+// 2 x M/2 eight-byte reads per pair.  Each output's sum runs t = M/2 - 1 .. 0 as in the
+// one-pair form (bit-identical).
+template <bool FMA, int M, int KIND>
+__device__ __forceinline__ void rev_two_pairs(const double* buf, int half, int u, const Filters& f,
+                                              d2& o0, d2& o1) {
+  constexpr int T2 = M / 2;
+  constexpr int LO = (T2 & 1) ? T2 - 1 : T2;  // base u - LO: even, <= u - T2 + 1
+  constexpr int NV = (LO + 2) / 2;            // 16-byte pairs covering [u - LO, u + 1]
+  double a[2 * NV], d[2 * NV];
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    const d2 va = *(const d2*)&buf[u - LO + 2 * q];
+    const d2 vd = *(const d2*)&buf[u - LO + 2 * q + half];
+    a[2 * q] = va.x;
+    a[2 * q + 1] = va.y;
+    d[2 * q] = vd.x;
+    d[2 * q + 1] = vd.y;
+  }
+  double a0 = 0., a1 = 0., b0 = 0., b1 = 0.;
+#pragma unroll
+  for (int t = T2 - 1; t >= 0; --t) {
+    const int i = LO - t;  // buf[u - t] at a[LO - t], buf[u + 1 - t] at a[LO - t + 1]
+    a0 = rev_acc<FMA, KIND>(a0, a[i], d[i], f.sR[2 * t], f.wR[2 * t]);
+    a1 = rev_acc<FMA, KIND>(a1, a[i], d[i], f.sR[2 * t + 1], f.wR[2 * t + 1]);
+    b0 = rev_acc<FMA, KIND>(b0, a[i + 1], d[i + 1], f.sR[2 * t], f.wR[2 * t]);
+    b1 = rev_acc<FMA, KIND>(b1, a[i + 1], d[i + 1], f.sR[2 * t + 1], f.wR[2 * t + 1]);
+  }
+  o0 = d2{a0, a1};
+  o1 = d2{b0, b1};
+}
+
 template <bool FMA, int M, int KIND, int H>
 __device__ __forceinline__ void row_rev_level(double* buf, double* xs, int tid, const Filters& f,
                                               const d2* tp) {
   constexpr int half = H / 2, P = half >= kNT2 ? half / kNT2 : 1;
   d2 o[P];
+  if constexpr (FMA && H >= M && P >= 2 && kRevPairs2) {
+    // lanes take pairs (2v, 2v + 1), v = tid + r kNT2; the wave holding the wrapped pairs
+    // (u < M/2 - 1, r = 0, tid < 64) keeps the one-pair forms.  FMA contract only: in STRICT
+    // (four FP64 instructions per tap instead of two) the blocked form measured slower, 5.08 ->
+    // 5.24 ms per cfg4 reverse, against 3.67 -> 3.37 ms with FMA (profiles/r03/ab_revpairs.log)
+#pragma unroll
+    for (int r = 0; r < P / 2; ++r) {
+      const int u = 2 * (tid + r * kNT2);
+      if (r == 0 && tid < 64) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int ue = u + e;
+          if constexpr (FMA) {
+            double a0 = 0., a1 = 0.;
+#pragma unroll
+            for (int t = (M >> 1) - 1; t >= 0; --t) {
+              const int i = (ue - t) & (half - 1);
+              const double av = buf[i], dv = buf[i + half];
+              a0 = rev_acc<FMA, KIND>(a0, av, dv, f.sR[2 * t], f.wR[2 * t]);
+              a1 = rev_acc<FMA, KIND>(a1, av, dv, f.sR[2 * t + 1], f.wR[2 * t + 1]);
+            }
+            o[2 * r + e] = d2{a0, a1};
+          } else {
+            o[2 * r + e] = rev_pair_rot<FMA, M, KIND>(buf, H, ue, tp);
+          }
+        }
+      } else {
+        rev_two_pairs<FMA, M, KIND>(buf, half, u, f, o[2 * r], o[2 * r + 1]);
+      }
+    }
+    if constexpr (H == kRowN) {  // last level: straight to global memory
+#pragma unroll
+      for (int r = 0; r < P / 2; ++r) {
+        const int u = 2 * (tid + r * kNT2);
+        *(d2*)&xs[2 * u] = o[2 * r];
+        *(d2*)&xs[2 * u + 2] = o[2 * r + 1];
+      }
+      return;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < P / 2; ++r) {
+      const int u = 2 * (tid + r * kNT2);
+      *(d2*)&buf[2 * u] = o[2 * r];
+      *(d2*)&buf[2 * u + 2] = o[2 * r + 1];
+    }
+    __syncthreads();
+    return;
+  }
   if constexpr (H < M) {  // multi-wrap: Java's loop replayed per output
     if (tid < half) o[0] = rev_pair_wrapped<FMA, M, KIND>(buf, H, tid, f);
   } else {
