@@ -117,10 +117,10 @@ __device__ __forceinline__ void bstore2(rsrc_t r, int off, d2 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, CP);
 }
 
-template <int L, int J, bool FMA, int NT, int SCP, class Fetch>
+template <int L, int J, bool FMA, int NT, int SCP, bool ONE, class Fetch>
 __device__ __forceinline__ void fwd_step(double* lds, d2& cur, Fetch&& fetch, long a, long P,
-                                         long seg_end, const rsrc_t (&rw)[J + 1],
-                                         const Taps& taps) {
+                                         long seg_end, const rsrc_t (&rw)[ONE ? 1 : J + 1],
+                                         int n8, const Taps& taps) {
   constexpr int C = 2 * NT;
   using G = GeoF<L, J, C>;
   const int t = threadIdx.x;
@@ -129,7 +129,10 @@ __device__ __forceinline__ void fwd_step(double* lds, d2& cur, Fetch&& fetch, lo
   fetch(cur);  // the chunk two steps ahead: in flight behind this step and the next
   __syncthreads();
   const long pos = a + i;
-  const int off = (pos >= P && pos < seg_end) ? (int)(pos * 8) : kOOB;  // P, seg_end even
+  const bool in = pos >= P && pos < seg_end;  // P, seg_end even
+  const int off = in ? (int)(pos * 8) : kOOB;
+  // row r's store offset: its own resource (off), or the one all-rows resource (r N 8 further)
+  auto roff = [&](int r) -> int { return ONE ? (in ? off + r * n8 : kOOB) : off; };
 #pragma unroll
   for (int j = 1; j <= J; ++j) {
     const int d = 1 << (j - 1);
@@ -159,11 +162,11 @@ __device__ __forceinline__ void fwd_step(double* lds, d2& cur, Fetch&& fetch, lo
         v1 = madd<FMA>(v1, taps.a[m], pr.y);
       }
     }
-    bstore2<SCP>(rw[j - 1], off, d2{w0, w1});
+    bstore2<SCP>(rw[ONE ? 0 : j - 1], roff(j - 1), d2{w0, w1});
     if (j < J) {
       *(d2*)&lds[G::cs(j + 1) + i] = d2{v0, v1};
     } else {
-      bstore2<SCP>(rw[J], off, d2{v0, v1});
+      bstore2<SCP>(rw[ONE ? 0 : J], roff(J), d2{v0, v1});
     }
     __syncthreads();
   }
@@ -186,8 +189,11 @@ __device__ __forceinline__ void fwd_step(double* lds, d2& cur, Fetch&& fetch, lo
   }
 }
 
-// SCP: cache-policy bits of the coefficient stores (A/B microbenchmarks; 0 in the product)
-template <int L, int J, bool FMA, int NT, int SCP = 0>
+// SCP: cache-policy bits of the coefficient stores (A/B microbenchmarks; 0 in the product).
+// ONE: the J + 1 coefficient rows through one buffer resource (the launch picks it when
+// (J + 1) N 8 < kOOB): 4 SGPRs instead of 4 (J + 1); sym8 J=6 spilled 44 SGPRs with a resource
+// per row.
+template <int L, int J, bool FMA, int NT, int SCP = 0, bool ONE = false>
 __global__ __launch_bounds__(NT) void modwt_fwd_fast(const double* __restrict__ x,
                                                      double* __restrict__ coeffs, long N,
                                                      long seg_len, long warm, long npairs,
@@ -201,9 +207,14 @@ __global__ __launch_bounds__(NT) void modwt_fwd_fast(const double* __restrict__ 
   const double* xs = x + (long)blockIdx.y * N;
   double* cs = coeffs + (long)blockIdx.y * (long)(J + 1) * N;
   const rsrc_t rx = make_rsrc(xs, N);
-  rsrc_t rw[J + 1];
+  rsrc_t rw[ONE ? 1 : J + 1];
+  if constexpr (ONE) {
+    rw[0] = make_rsrc(cs, (long)(J + 1) * N);
+  } else {
 #pragma unroll
-  for (int j = 0; j <= J; ++j) rw[j] = make_rsrc(cs + (long)j * N, N);
+    for (int j = 0; j <= J; ++j) rw[j] = make_rsrc(cs + (long)j * N, N);
+  }
+  const int n8 = (int)(N * 8);  // row stride in bytes (used when ONE)
   for (int i = t; i < G::total; i += NT) lds[i] = 0.0;
 
   long a = P - warm;
@@ -228,9 +239,9 @@ __global__ __launch_bounds__(NT) void modwt_fwd_fast(const double* __restrict__ 
   for (int k = 0; k < 2 * (J + 1); ++k) bstore(rx, kOOB - 8 * k, 0.0);  // distinct: not merged
   __syncthreads();
   for (long k = 0; k < npairs; ++k) {
-    fwd_step<L, J, FMA, NT, SCP>(lds, A, fetch, a, P, seg_end, rw, taps);
+    fwd_step<L, J, FMA, NT, SCP, ONE>(lds, A, fetch, a, P, seg_end, rw, n8, taps);
     a += C;
-    fwd_step<L, J, FMA, NT, SCP>(lds, B, fetch, a, P, seg_end, rw, taps);
+    fwd_step<L, J, FMA, NT, SCP, ONE>(lds, B, fetch, a, P, seg_end, rw, n8, taps);
     a += C;
   }
 }
@@ -559,6 +570,10 @@ int launch_fwd(const Taps& t, const double* x, double* c, long N, int batch, hip
   const long npairs = ((seg + warm) / C + 1) / 2;  // an odd extra step runs right of the segment
   const size_t lds = (size_t)G::total * sizeof(double);
   const long cs = (long)(J + 1) * N;
+  const char* g1 = std::getenv("JW_FWD_ONE_RSRC");  // A/B runs: 0 = one resource per row
+  if (cs * 8 < (long)kOOB && !(g1 && g1[0] == '0'))
+    return launch(modwt_fwd_fast<L, J, FMA, NT, 0, true>, lds, nseg, batch, NT, s, x, N, c, cs, N,
+                  seg, warm, npairs, t);
   return launch(modwt_fwd_fast<L, J, FMA, NT>, lds, nseg, batch, NT, s, x, N, c, cs, N, seg, warm,
                 npairs, t);
 }

@@ -175,7 +175,11 @@ struct HP : HistP<L, J, JL> {
 
 // D register sets of prefetched coefficients (step s uses set s % D), U steps unrolled per
 // loop trip (a multiple of D).  MEM = 0 (microbenchmarks only): no HBM traffic.
-template <int L, int J, bool FMA, int D, int U, int MEM = 1>
+// ONE: every coefficient row through one buffer resource (row r at byte (r N + p) 8; the
+// launch picks it when (J + 1) N 8 < 2^31) instead of one resource per row: 4 SGPRs instead of
+// 4 (J + 1), which for sym8 J=6 cuts the SGPR spills (to VGPR lanes, read back per tap use)
+// from 92 to 18.
+template <int L, int J, bool FMA, int D, int U, int MEM = 1, bool ONE = false>
 __global__ __launch_bounds__(64) void modwt_inv_wave2(const double* __restrict__ coeffs,
                                                       double* __restrict__ x, long N, long seg_len,
                                                       long a_start, long ngroups, Taps taps) {
@@ -190,9 +194,16 @@ __global__ __launch_bounds__(64) void modwt_inv_wave2(const double* __restrict__
   const long seg_end = min(P + seg_len, N);
   const double* cs = coeffs + (long)blockIdx.y * (long)(J + 1) * N;
   const rsrc_t rx = make_rsrc(x + (long)blockIdx.y * N, N);
-  rsrc_t rc[J + 1];
+  rsrc_t rc[ONE ? 1 : J + 1];
+  if constexpr (ONE) {
+    rc[0] = make_rsrc(cs, (long)(J + 1) * N);
+  } else {
 #pragma unroll
-  for (int j = 0; j <= J; ++j) rc[j] = make_rsrc(cs + (long)j * N, N);
+    for (int j = 0; j <= J; ++j) rc[j] = make_rsrc(cs + (long)j * N, N);
+  }
+  // byte offset of position p (< N) of coefficient row `row`
+  auto roff = [&](int row, long p) -> int { return (int)((ONE ? p + (long)row * N : p) * 8); };
+  auto rrs = [&](int row) -> rsrc_t { return rc[ONE ? 0 : row]; };
   for (int i = lane; i < G::lds_doubles / 2; i += 64) lds[i] = d2{0.0, 0.0};
   d2 rg[GW::rtot];
 #pragma unroll
@@ -213,7 +224,7 @@ __global__ __launch_bounds__(64) void modwt_inv_wave2(const double* __restrict__
     auto ld = [&](int row, int k) -> double {
       long p = lb + k;
       p = p >= N ? p - N : p;
-      return MEM ? bload(rc[row], (int)(p * 8)) : (double)(p + row);
+      return MEM ? bload(rrs(row), roff(row, p)) : (double)(p + row);
     };
     [&]<int... js>(std::integer_sequence<int, js...>) {
       (([&] {
@@ -228,7 +239,7 @@ __global__ __launch_bounds__(64) void modwt_inv_wave2(const double* __restrict__
     if constexpr (!G::TOPREG) {
       long p2 = lb + 2 * lane;
       p2 = p2 >= N ? p2 - N : p2;
-      dst.vtop = MEM ? bload2(rc[J], (int)(p2 * 8)) : d2{(double)p2, (double)(p2 + 1)};
+      dst.vtop = MEM ? bload2(rrs(J), roff(J, p2)) : d2{(double)p2, (double)(p2 + 1)};
     }
 #pragma unroll
     for (int e = 0; e < 2; ++e)
@@ -328,7 +339,9 @@ int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hip
   const long ngroups = steps / U;
   const long a_start = (steps - 1) * kS;
   const size_t lds = (size_t)G::lds_doubles * sizeof(double);
-  auto kern = modwt_inv_wave2<L, J, FMA, D, U>;
+  const char* g1 = std::getenv("JW_INV_ONE_RSRC");  // A/B runs: 0 = one resource per row
+  const bool one = (long)(J + 1) * N * 8 < 0x7fffffffL && !(g1 && g1[0] == '0');
+  auto kern = one ? modwt_inv_wave2<L, J, FMA, D, U, 1, true> : modwt_inv_wave2<L, J, FMA, D, U>;
   JW_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)lds));
   const long cstride = (long)(J + 1) * N;
