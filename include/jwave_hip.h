@@ -25,7 +25,11 @@
  *     allocation would fail, and on jw_release_caches();
  *   - per host thread and device, three non-blocking streams and a ring of three 32 MiB pinned
  *     bounce buffers per direction (192 MiB) for JW_HOST staging, freed when the thread exits
- *     (JW_PIN_RING / JW_PIN_MB / JW_COPY_THREADS tune them).
+ *     (JW_PIN_RING / JW_PIN_MB / JW_COPY_THREADS tune them);
+ *   - per host thread and device, one more non-blocking stream and two events on which
+ *     jw_cwt_fft runs its one-pass (band) scales beside the two-pass ones, forked from and
+ *     joined back into the caller's stream by events (stream order for the caller is
+ *     unchanged; JW_CWT_OVERLAP=0 keeps the whole call on the caller's stream).
  */
 #ifndef JWAVE_HIP_H
 #define JWAVE_HIP_H
