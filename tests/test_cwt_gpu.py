@@ -229,3 +229,41 @@ def test_fft_scalogram_fused(device):
     ed = t.transformFFTScalogram(torch.from_numpy(xs).to(device), scales)
     assert ed.is_cuda and np.array_equal(ed.cpu().numpy(), e)
     assert np.array_equal(t.transformFFTScalogram(np.zeros((2, 0)), scales), np.zeros((2, 11)))
+
+
+def test_concurrent_host_threads_with_side_streams():
+    # Host arrays (JW_HOST) from four threads at once: each thread stages on its own streams
+    # and runs its band scales on its own side stream (forked from and joined into its staging
+    # stream).  Every thread's result equals the same call made alone, bit for bit, and with
+    # the side stream off (JW_CWT_OVERLAP=0: the same kernels on one stream).
+    import os
+    import threading
+    n = 1 << 16
+    scales = CWT.generateLogScales(2.0, 1024.0, 16)
+    xs = [orc.fill_uniform(n, 100 + i) for i in range(4)]
+    alone = [CWT(MorletWavelet(*MORLET6)).transformFFT(x, scales, 1.0).getCoefficients()
+             for x in xs]
+    got = [None] * 4
+    errs = []
+
+    def work(i):
+        try:
+            for _ in range(3):
+                got[i] = CWT(MorletWavelet(*MORLET6)).transformFFT(xs[i], scales, 1.0).getCoefficients()
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
+    for i in range(4):
+        assert np.array_equal(got[i], alone[i]), i
+    os.environ["JW_CWT_OVERLAP"] = "0"
+    try:
+        one = CWT(MorletWavelet(*MORLET6)).transformFFT(xs[0], scales, 1.0).getCoefficients()
+    finally:
+        del os.environ["JW_CWT_OVERLAP"]
+    assert np.array_equal(one, alone[0])
