@@ -165,6 +165,28 @@ def test_inverse_wave_vs_workgroup_bit_exact(wname, n, J, kernel, monkeypatch):
         assert bits_equal(got[b], orc.modwt_inverse(c * k, g, h, "direct_nz"))
 
 
+@pytest.mark.parametrize("one", ["0", "1"])
+@pytest.mark.parametrize("wname,n,J", [("Daubechies4", 1 << 15, 8), ("Symlet8", 70002, 6),
+                                       ("Daubechies8", 5000, 7), ("Haar1", 4098, 10)])
+def test_row_resource_forms_bit_exact(wname, n, J, one, monkeypatch):
+    # The fused kernels address the J + 1 coefficient rows through one buffer resource when
+    # they fit (JW_FWD_ONE_RSRC / JW_INV_ONE_RSRC = 1, the default) or one per row (0): the
+    # same loads and stores, so both equal the oracle bit for bit (and the tail stores past a
+    # segment stay dropped in both).
+    wv = W.by_name(wname)
+    g, h = ofilters(wv)
+    x = orc.fill_uniform(n, 31 + n)
+    monkeypatch.setenv("JW_FWD_ONE_RSRC", one)
+    monkeypatch.setenv("JW_INV_ONE_RSRC", one)
+    ref = orc.modwt_forward(x, J, g, h, "direct_nz")
+    for kernel in ("wave2", "wave"):
+        monkeypatch.setenv("JW_INV_KERNEL", kernel)
+        m = direct(wv)
+        c = m.forwardMODWT(x, J)
+        assert bits_equal(c, ref)
+        assert bits_equal(m.inverseMODWT(c), orc.modwt_inverse(ref, g, h, "direct_nz"))
+
+
 @pytest.mark.parametrize("wname,n,J", [("Haar1", 64, 6), ("Daubechies4", 100, 5),
                                        ("Symlet8", 8, 3), ("Daubechies8", 300, 4)])
 def test_strict_bit_exact_vs_faithful_oracle(wname, n, J):
