@@ -190,8 +190,10 @@ __global__ __launch_bounds__(64) void modwt_inv_wave2(const double* __restrict__
   constexpr int NR = G::TOPREG ? J - 4 : 0;  // rows in 64-lane sub-step form: W_6..W_J, V_J
   extern __shared__ __attribute__((aligned(16))) d2 lds[];
   const int lane = threadIdx.x;
-  const long P = (long)blockIdx.x * seg_len;
-  const long seg_end = min(P + seg_len, N);
+  // positions in 32 bits (N < 2^28: the byte offsets below are 32-bit already), fewer SGPRs
+  const int Ni = (int)N;
+  const int P = (int)(blockIdx.x * seg_len);
+  const int seg_end = min(P + (int)seg_len, Ni);
   const double* cs = coeffs + (long)blockIdx.y * (long)(J + 1) * N;
   const rsrc_t rx = make_rsrc(x + (long)blockIdx.y * N, N);
   rsrc_t rc[ONE ? 1 : J + 1];
@@ -202,7 +204,7 @@ __global__ __launch_bounds__(64) void modwt_inv_wave2(const double* __restrict__
     for (int j = 0; j <= J; ++j) rc[j] = make_rsrc(cs + (long)j * N, N);
   }
   // byte offset of position p (< N) of coefficient row `row`
-  auto roff = [&](int row, long p) -> int { return (int)((ONE ? p + (long)row * N : p) * 8); };
+  auto roff = [&](int row, int p) -> int { return (ONE ? p + row * Ni : p) * 8; };
   auto rrs = [&](int row) -> rsrc_t { return rc[ONE ? 0 : row]; };
   for (int i = lane; i < G::lds_doubles / 2; i += 64) lds[i] = d2{0.0, 0.0};
   d2 rg[GW::rtot];
@@ -213,8 +215,8 @@ __global__ __launch_bounds__(64) void modwt_inv_wave2(const double* __restrict__
   for (int i = 0; i < GW::NX; ++i) xr[i] = zr[i] = d2{0.0, 0.0};
   HP<L, J, JL> hp;
 
-  long a = P + a_start;  // chunk start of the current step (may exceed N: taken mod N)
-  long lb = a % N;       // load cursor: chunk start (mod N) of the next fetch
+  int a = P + (int)a_start;  // chunk start of the current step (may exceed N: taken mod N)
+  int lb = a % Ni;           // load cursor: chunk start (mod N) of the next fetch
   struct Set {
     double w[JL][2];                // W_j at the lane's V_j positions (v_positions), j = 1..JL
     d2 vtop;                        // V_J pair at a + 2l when J <= 5
@@ -222,8 +224,8 @@ __global__ __launch_bounds__(64) void modwt_inv_wave2(const double* __restrict__
   };
   auto fetch = [&](Set& dst) {
     auto ld = [&](int row, int k) -> double {
-      long p = lb + k;
-      p = p >= N ? p - N : p;
+      int p = lb + k;
+      p = p >= Ni ? p - Ni : p;
       return MEM ? bload(rrs(row), roff(row, p)) : (double)(p + row);
     };
     [&]<int... js>(std::integer_sequence<int, js...>) {
@@ -237,8 +239,8 @@ __global__ __launch_bounds__(64) void modwt_inv_wave2(const double* __restrict__
        ...);
     }(std::make_integer_sequence<int, JL>{});
     if constexpr (!G::TOPREG) {
-      long p2 = lb + 2 * lane;
-      p2 = p2 >= N ? p2 - N : p2;
+      int p2 = lb + 2 * lane;
+      p2 = p2 >= Ni ? p2 - Ni : p2;
       dst.vtop = MEM ? bload2(rrs(J), roff(J, p2)) : d2{(double)p2, (double)(p2 + 1)};
     }
 #pragma unroll
@@ -246,7 +248,7 @@ __global__ __launch_bounds__(64) void modwt_inv_wave2(const double* __restrict__
 #pragma unroll
       for (int i = 0; i < NR; ++i) dst.r[i][e] = ld(5 + i, 64 * e + lane);
     lb -= kS;
-    if (lb < 0) lb += N;
+    if (lb < 0) lb += Ni;
   };
   Set S[D];
 #pragma unroll
@@ -256,7 +258,7 @@ __global__ __launch_bounds__(64) void modwt_inv_wave2(const double* __restrict__
   }
   wave_lds_sync();
 
-  for (long gi = 0; gi < ngroups; ++gi) {
+  for (int gi = 0; gi < (int)ngroups; ++gi) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       fetch(S[(u + D - 1) % D]);
@@ -303,7 +305,7 @@ __global__ __launch_bounds__(64) void modwt_inv_wave2(const double* __restrict__
         v[1] = cur.vtop.y;
       }
       LdsLevels<L, J, FMA, JL>::run(lds, lane, taps, v, cur.w, hp);
-      const long pos = a + 2 * lane;
+      const int pos = a + 2 * lane;
       bstore2(rx, (MEM && pos >= P && pos < seg_end) ? (int)(pos * 8) : kOOB, d2{v[0], v[1]});
       a -= kS;
     }
