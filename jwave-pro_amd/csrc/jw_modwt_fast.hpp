@@ -118,8 +118,8 @@ __device__ __forceinline__ void bstore2(rsrc_t r, int off, d2 v) {
 }
 
 template <int L, int J, bool FMA, int NT, int SCP, bool ONE, class Fetch>
-__device__ __forceinline__ void fwd_step(double* lds, d2& cur, Fetch&& fetch, long a, long P,
-                                         long seg_end, const rsrc_t (&rw)[ONE ? 1 : J + 1],
+__device__ __forceinline__ void fwd_step(double* lds, d2& cur, Fetch&& fetch, int a, int P,
+                                         int seg_end, const rsrc_t (&rw)[ONE ? 1 : J + 1],
                                          int n8, const Taps& taps) {
   constexpr int C = 2 * NT;
   using G = GeoF<L, J, C>;
@@ -128,9 +128,9 @@ __device__ __forceinline__ void fwd_step(double* lds, d2& cur, Fetch&& fetch, lo
   *(d2*)&lds[G::cs(1) + i] = cur;
   fetch(cur);  // the chunk two steps ahead: in flight behind this step and the next
   __syncthreads();
-  const long pos = a + i;
+  const int pos = a + i;  // may be negative in the warm-up (then out of range)
   const bool in = pos >= P && pos < seg_end;  // P, seg_end even
-  const int off = in ? (int)(pos * 8) : kOOB;
+  const int off = in ? pos * 8 : kOOB;
   // row r's store offset: its own resource (off), or the one all-rows resource (r N 8 further)
   auto roff = [&](int r) -> int { return ONE ? (in ? off + r * n8 : kOOB) : off; };
 #pragma unroll
@@ -202,8 +202,11 @@ __global__ __launch_bounds__(NT) void modwt_fwd_fast(const double* __restrict__ 
   constexpr int C = 2 * NT;
   using G = GeoF<L, J, C>;
   const int t = threadIdx.x;
-  const long P = (long)blockIdx.x * seg_len;
-  const long seg_end = min(P + seg_len, N);
+  // stream positions in 32 bits (N < 2^27, see kOOB; the warm-up starts at most one segment
+  // plus warm before 0)
+  const int Ni = (int)N;
+  const int P = (int)(blockIdx.x * seg_len);
+  const int seg_end = min(P + (int)seg_len, Ni);
   const double* xs = x + (long)blockIdx.y * N;
   double* cs = coeffs + (long)blockIdx.y * (long)(J + 1) * N;
   const rsrc_t rx = make_rsrc(xs, N);
@@ -217,15 +220,15 @@ __global__ __launch_bounds__(NT) void modwt_fwd_fast(const double* __restrict__ 
   const int n8 = (int)(N * 8);  // row stride in bytes (used when ONE)
   for (int i = t; i < G::total; i += NT) lds[i] = 0.0;
 
-  long a = P - warm;
-  long lb = a % N;  // load cursor: stream position of the next chunk to fetch, mod N (even)
-  if (lb < 0) lb += N;
+  int a = P - (int)warm;
+  int lb = a % Ni;  // load cursor: stream position of the next chunk to fetch, mod N (even)
+  if (lb < 0) lb += Ni;
   auto fetch = [&](d2& dst) {
-    long p = lb + 2 * t;
-    p = p >= N ? p - N : p;
-    dst = bload2(rx, (int)(p * 8));
+    int p = lb + 2 * t;
+    p = p >= Ni ? p - Ni : p;
+    dst = bload2(rx, p * 8);
     lb += C;
-    if (lb >= N) lb -= N;
+    if (lb >= Ni) lb -= Ni;
   };
   d2 A, B;
   fetch(A);
@@ -238,7 +241,7 @@ __global__ __launch_bounds__(NT) void modwt_fwd_fast(const double* __restrict__ 
 #pragma unroll
   for (int k = 0; k < 2 * (J + 1); ++k) bstore(rx, kOOB - 8 * k, 0.0);  // distinct: not merged
   __syncthreads();
-  for (long k = 0; k < npairs; ++k) {
+  for (int k = 0; k < (int)npairs; ++k) {
     fwd_step<L, J, FMA, NT, SCP, ONE>(lds, A, fetch, a, P, seg_end, rw, n8, taps);
     a += C;
     fwd_step<L, J, FMA, NT, SCP, ONE>(lds, B, fetch, a, P, seg_end, rw, n8, taps);
