@@ -99,8 +99,10 @@ __global__ __launch_bounds__(kW) void modwt_inv_wave(const double* __restrict__ 
   constexpr int JL = G::JL;
   extern __shared__ __attribute__((aligned(16))) d2 lds2[];
   const int lane = threadIdx.x;
-  const long P = (long)blockIdx.x * seg_len;
-  const long seg_end = min(P + seg_len, N);
+  // stream positions in 32 bits (N < 2^27 on this path, see kOOB)
+  const int Ni = (int)N;
+  const int P = (int)(blockIdx.x * seg_len);
+  const int seg_end = min(P + (int)seg_len, Ni);
   const double* cs = coeffs + (long)blockIdx.y * (long)(J + 1) * N;
   const rsrc_t rx = make_rsrc(x + (long)blockIdx.y * N, N);
   rsrc_t rc[J + 1];
@@ -118,18 +120,18 @@ __global__ __launch_bounds__(kW) void modwt_inv_wave(const double* __restrict__ 
 #pragma unroll
   for (int i = 0; i < (G::htot > 0 ? G::htot : 1); ++i) hp[i] = d2{0.0, 0.0};
 
-  long a = P + a_start;  // chunk start of the current step (>= 0, may exceed N: taken mod N)
-  long lb = a % N;       // load cursor: chunk start (mod N) of the next fetch
+  int a = P + (int)a_start;  // chunk start of the current step (>= 0, may exceed N: mod N)
+  int lb = a % Ni;           // load cursor: chunk start (mod N) of the next fetch
   auto fetch = [&](double (&dst)[J + 1]) {
-    long p = lb + lane;
-    p = p >= N ? p - N : p;
-    const int off = (int)(p * 8);
+    int p = lb + lane;
+    p = p >= Ni ? p - Ni : p;
+    const int off = p * 8;
 #pragma unroll
     for (int j = 0; j <= J; ++j)
       dst[j] = MEM ? __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rc[j], off, 0, CP))
                    : (double)(p + j);
     lb -= kW;
-    if (lb < 0) lb += N;
+    if (lb < 0) lb += Ni;
   };
   double S[D][J + 1];
 #pragma unroll
@@ -139,7 +141,7 @@ __global__ __launch_bounds__(kW) void modwt_inv_wave(const double* __restrict__ 
   }
   wave_lds_sync();
 
-  for (long g = 0; g < ngroups; ++g) {
+  for (int g = 0; g < (int)ngroups; ++g) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       fetch(S[(u + D - 1) % D]);  // the set consumed at step u-1: refilled for step u+D-1
@@ -204,8 +206,8 @@ __global__ __launch_bounds__(kW) void modwt_inv_wave(const double* __restrict__ 
             base[o + kW * (k + 1)] = hp[ho + k];
         }
       }
-      const long pos = a + lane;
-      bstore(rx, (MEM && pos >= P && pos < seg_end) ? (int)(pos * 8) : kOOB, v);
+      const int pos = a + lane;
+      bstore(rx, (MEM && pos >= P && pos < seg_end) ? pos * 8 : kOOB, v);
       a -= kW;
     }
   }
