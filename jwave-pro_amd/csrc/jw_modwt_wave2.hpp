@@ -322,12 +322,13 @@ constexpr bool inv_ok() {
 // Default choice over the one-output wave kernel (jw_modwt_wave.hpp), from the A/B runs at
 // N = 2^20 x 1024 on random data (tools/micro/invwave2.hip, profiles/r03/invwave2_*.log):
 // sym8 J6 19.5 -> 16.3 ms (FMA) and 23.5 -> 21.0 ms (STRICT), sym8 J7 24.0 -> 21.7 ms, db4 J6
-// and J4 1-2 % faster; db4 J8 ties in FMA (16.8 vs 16.9 ms) but loses in STRICT (19.0 vs 17.4 ms):
-// with the two register levels of J >= 8 it needs 262 VGPRs, one wave per SIMD (forcing two
-// waves spills: 21 ms).
+// and J4 1-2 % faster; db4 J8 tied in FMA (16.8 vs 16.9 ms) and lost in STRICT (19.0 vs 17.4 ms)
+// while the two register levels of J >= 8 needed 262 VGPRs, one wave per SIMD.  With 32-bit
+// stream positions it fits 246 VGPRs, two waves per SIMD, and db4 J8 STRICT wins too: 17.5 vs
+// 17.9-18.1 ms (profiles/r03/inv_kernel_choice.log).
 template <int L, int J, bool FMA>
 constexpr bool inv_prefer2() {
-  return J <= 7 || (FMA && L <= 8);
+  return J <= 7 || L <= 8;
 }
 
 template <int L, int J, bool FMA, int D = 2, int U = 2>
