@@ -121,7 +121,7 @@ def inv_kernel_name(L, J, n, arith="fma"):
         lds2 += 2 * half * 16
     wave2 = (n % 2 == 0 and lds2 <= 20 * 1024 and
              (rtot if J >= 7 else 0) + (nx_nz if J >= 6 else 0) <= 31)
-    prefer2 = J <= 7 or (arith == "fma" and L <= 8)
+    prefer2 = J <= 7 or L <= 8  # jw_modwt_wave2.hpp inv_prefer2 (both contracts)
     if env == "wg":
         return "modwt_inv_fast"
     if wave2 and (env == "wave2" or (env not in ("wave", "wave1") and (prefer2 or not wave1))):
@@ -558,6 +558,25 @@ def main():
                 "note": "jw_modwt_forward + jw_modwt_inverse with where=JW_HOST (host arrays "
                         "in and out, DIRECT), PCIe staging included; never the headline value",
                 "recon_max_abs": float(np.max(np.abs(xrh - xh)))}
+        # the reference API's own unit (MODWTTransform.java:256,337; the JNI nForward/nInverse):
+        # one signal per call, host arrays in and out
+        x1, c1, xr1 = xh[:1].copy(), np.empty((1, J + 1, n)), np.empty((1, n))
+
+        def one_step():
+            _native.check(lib.jw_modwt_forward(hplan, P(x1), P(c1), n, J, 1, _native.JW_CONV_DIRECT,
+                                               _native.JW_HOST, None))
+            _native.check(lib.jw_modwt_inverse(hplan, P(c1), P(xr1), n, J, 1, _native.JW_CONV_DIRECT,
+                                               _native.JW_HOST, None))
+
+        one_step()
+        t0 = time.perf_counter()
+        for _ in range(4 * reps):
+            one_step()
+        t1 = (time.perf_counter() - t0) / (4 * reps)
+        host["one_signal"] = {"value": round(n / t1 / 1e6, 1), "unit": "Msamples/s",
+                              "ms_per_call_pair": round(t1 * 1e3, 3),
+                              "note": "batch 1 per call (the reference API's unit; JNI nForward + "
+                                      "nInverse), host arrays, PCIe staging included"}
         ca = torch.empty((nb, J + 1, n), dtype=torch.float64, device=dev)
         xra = torch.empty((nb, n), dtype=torch.float64, device=dev)
 

@@ -44,7 +44,8 @@ extern "C" {
 #define JW_ERR_FAILURE (-2)          /* JWaveFailure */
 #define JW_ERR_DEVICE (-3)           /* HIP runtime / kernel launch error */
 #define JW_ERR_NO_MEMORY (-4)
-#define JW_ERR_UNSUPPORTED (-5)
+#define JW_ERR_UNSUPPORTED (-5)      /* UnsupportedOperationException: a length or mode this
+                                        engine does not run (the message names the limit) */
 
 /* ---- where the caller's buffers live ---- */
 #define JW_HOST 0   /* host memory: the call stages through HBM and synchronises */
@@ -106,12 +107,16 @@ int jw_modwt_plan_filters(const jw_modwt_plan* plan, double* g, double* h);
  * reference's performConvolution takes (:640-664): FFT always, DIRECT never, AUTO when the
  * int32 product n * M_j > fftConvolutionThreshold (M_j = (L-1) 2^(j-1) + 1, wrap included).
  * DIRECT levels are bit-identical to circularConvolve (:677-690).  FFT levels run the
- * reference's circularConvolveFFT (:752-786) with its own FFT (FastFourierTransform.java
- * :172-212), bit-identical to the JVM for power-of-two 2 <= n <= 2^23; other n run the
- * exact-twiddle chirp-z pyramid (within 1e-10 of DIRECT).
+ * reference's circularConvolveFFT (:752-786) with its own FFT: radix 2 with recurrence
+ * twiddles for powers of two (FastFourierTransform.java:172-212) and its Bluestein transform for
+ * other lengths (:259-324), both bit-identical to the JVM for 2 <= n <= 2^23 -- given that the
+ * JVM's Math.sin/Math.cos are correctly rounded at the twiddle and chirp angles (Java specifies
+ * them to 1 ulp; the engine and the oracle both take the correctly rounded value).
  * With a JW_ARITH_FMA plan (the fast contract) FFT runs the exact-twiddle frequency-domain
  * pyramid for 2 <= n <= 2^23 (within 1e-10 of DIRECT); AUTO and DIRECT run the direct kernels
- * (faster and more accurate than any FFT path on this engine). */
+ * (faster and more accurate than any FFT path on this engine).
+ * A call with an FFT level (FFT, or AUTO's rule) at n > 2^23 returns JW_ERR_UNSUPPORTED naming
+ * the limit (never DIRECT values in its place); DIRECT runs any n. */
 int jw_modwt_forward(const jw_modwt_plan* plan, const double* x, double* coeffs, long n,
                      int levels, int batch, int method, int where, void* stream);
 /* inverseMODWT(coefficients) (:337-375): coeffs batch x (levels+1) x n -> x batch x n.
@@ -135,9 +140,11 @@ int jw_fft_reverse(const double* in_reim, double* out_reim, long n, int batch, i
                    void* stream);
 /* The same transforms under an arithmetic contract.  JW_ARITH_STRICT runs the reference's own
  * algorithm operation for operation -- bit reversal, radix-2 decimation in time with the
- * recurrence twiddles wn = wn.mul(w) of every stage (:172-212), Complex.mul's (ac - bd, ad + bc)
- * -- so results are the JVM's bit for bit for power-of-two n <= 2^24.  JW_ARITH_FMA is
- * jw_fft_forward / jw_fft_reverse (correctly rounded twiddle tables). */
+ * recurrence twiddles wn = wn.mul(w) of every stage (:172-212), Complex.mul's (ac - bd, ad + bc),
+ * Bluestein for other n (:259-324) -- so results are the JVM's bit for bit for power-of-two
+ * n <= 2^24 and other n <= 2^23 (correctly rounded Math.sin/cos assumed, as above); longer
+ * STRICT lines return JW_ERR_UNSUPPORTED.  JW_ARITH_FMA is jw_fft_forward / jw_fft_reverse
+ * (correctly rounded twiddle tables). */
 int jw_fft_forward_ex(const double* in_reim, double* out_reim, long n, int batch, int arith,
                       int where, void* stream);
 int jw_fft_reverse_ex(const double* in_reim, double* out_reim, long n, int batch, int arith,

@@ -121,6 +121,18 @@ public class HipContinuousWaveletTransform extends ContinuousWaveletTransform {
     return transform(signal, scales, samplingRate); // same values (:470-500)
   }
 
+  /**
+   * transformParallelCustom (ContinuousWaveletTransform.java:577-680) computes the same values
+   * as transform with a caller-sized ForkJoinPool; on the GPU the pool size has no meaning.
+   */
+  @Override
+  public CWTResult transformParallelCustom(double[] signal, double[] scales, double samplingRate,
+                                           int parallelism) {
+    if (kind() < 0)
+      return super.transformParallelCustom(signal, scales, samplingRate, parallelism);
+    return transform(signal, scales, samplingRate);
+  }
+
   private static native double[][] nTransformFFT(int kind, double[] params, double[] x,
                                                  double[] scales, double fs, int padding);
   private static native double[] nScalogramFFT(int kind, double[] params, double[] x,

@@ -75,6 +75,16 @@ public class HipFastWaveletTransform extends FastWaveletTransform {
     return line(1, arrHilb, level);
   }
 
+  private double[][][] space(int op, double[][][] x, int lvlP, int lvlQ, int lvlR)
+      throws JWaveException {
+    try {
+      if (device >= 0) HipEngine.setDevice(device);
+      return nSpace(plan, op, x, lvlP, lvlQ, lvlR);
+    } finally {
+      Reference.reachabilityFence(this);
+    }
+  }
+
   @Override
   public double[][] forward(double[][] matTime, int lvlM, int lvlN) throws JWaveException {
     return matrix(0, matTime, lvlM, lvlN);
@@ -85,6 +95,24 @@ public class HipFastWaveletTransform extends FastWaveletTransform {
     return matrix(1, matFreq, lvlM, lvlN);
   }
 
+  /**
+   * 3-D (BasicTransform.java:509-565): the 2-D forward of every slab with (lvlP, lvlQ), then the
+   * lines along the first dimension with lvlR.  The no-level overload (:487-495) passes
+   * getExponent of the three dimensions and reaches this override.
+   */
+  @Override
+  public double[][][] forward(double[][][] spcTime, int lvlP, int lvlQ, int lvlR)
+      throws JWaveException {
+    return space(0, spcTime, lvlP, lvlQ, lvlR);
+  }
+
+  /** 3-D reverse (BasicTransform.java:602-659), the reference's order. */
+  @Override
+  public double[][][] reverse(double[][][] spcHilb, int lvlP, int lvlQ, int lvlR)
+      throws JWaveException {
+    return space(1, spcHilb, lvlP, lvlQ, lvlR);
+  }
+
   static native long nPlanCreate(double[] sD, double[] wD, double[] sR, double[] wR,
                                  int motherWavelength, int transformWavelength, int kind,
                                  int arith);
@@ -93,4 +121,7 @@ public class HipFastWaveletTransform extends FastWaveletTransform {
   static native double[] nLine(long plan, int op, double[] x, int level) throws JWaveException;
   static native double[][] nMatrix(long plan, int op, double[][] x, int lvlM, int lvlN)
       throws JWaveException;
+  // op 0 forward, 1 reverse
+  static native double[][][] nSpace(long plan, int op, double[][][] x, int lvlP, int lvlQ,
+                                    int lvlR) throws JWaveException;
 }

@@ -141,7 +141,10 @@ public class HipMODWTTransform extends MODWTTransform {
         plan = null;
       }
     }
-    HipEngine.releaseCaches(); // the device-side tables (filter spectra, FFT twiddles)
+    // Per instance, as in the reference (MODWTTransform.java:556): only this object's plan is
+    // retired.  The process-wide device tables (twiddles, filter spectra, which are shared by
+    // every transform with the same taps and length) are freed only by an explicit
+    // HipEngine.releaseCaches(), which waits for every device and stalls other threads.
   }
 
   private static native long nPlanCreate(double[] scalDec, double[] wavDec, int fftThreshold,

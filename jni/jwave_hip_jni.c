@@ -209,6 +209,8 @@ JNIEXPORT jdoubleArray JNICALL Java_jwave_hip_HipMODWTTransform_nInverse(JNIEnv*
                                                                          jobjectArray coeffs,
                                                                          jint method) {
   (void)cls;
+  /* null, no rows or one row (no level): new double[0], as MODWTTransform.java:338-346 */
+  if (!coeffs || (*env)->GetArrayLength(env, coeffs) <= 1) return (*env)->NewDoubleArray(env, 0);
   jsize R = 0, n = 0;
   double* c = rows_in(env, coeffs, &R, &n);
   if (!c) return NULL;
@@ -343,6 +345,75 @@ JNIEXPORT jobjectArray JNICALL Java_jwave_hip_HipFastWaveletTransform_nMatrix(
                          : jw_fwt2d_reverse(p, x, y, rows, cols, lvlM, lvlN, 1, JW_HOST, NULL);
   free(x);
   jobjectArray out = st == JW_OK ? rows_out(env, y, rows, cols) : NULL;
+  free(y);
+  if (st != JW_OK) jw_throw(env, st);
+  return out;
+}
+
+/* 3-D: op 0 forward, 1 reverse (double[][][] spc, lvlP, lvlQ, lvlR), BasicTransform.java:509/:602.
+ * Every [d2][d3] slab must have the shape of the first one. */
+JNIEXPORT jobjectArray JNICALL Java_jwave_hip_HipFastWaveletTransform_nSpace(
+    JNIEnv* env, jclass cls, jlong plan, jint op, jobjectArray in, jint lvlP, jint lvlQ,
+    jint lvlR) {
+  (void)cls;
+  const jsize d1 = in ? (*env)->GetArrayLength(env, in) : 0;
+  jsize d2 = 0, d3 = 0;
+  double* x = NULL;
+  size_t slab = 0;
+  for (jsize i = 0; i < d1; ++i) {
+    jobjectArray m = (jobjectArray)(*env)->GetObjectArrayElement(env, in, i);
+    if ((*env)->ExceptionCheck(env)) {
+      free(x);
+      return NULL;
+    }
+    jsize r = 0, c = 0;
+    double* part = m ? rows_in(env, m, &r, &c) : NULL;
+    if (m) (*env)->DeleteLocalRef(env, m);
+    if (!part) {
+      free(x);
+      if (!(*env)->ExceptionCheck(env)) iae(env, "Space slabs must all have the same shape");
+      return NULL;
+    }
+    if (i == 0) {
+      d2 = r, d3 = c, slab = (size_t)d2 * d3;
+      x = malloc(sizeof(double) * (size_t)d1 * (slab ? slab : 1));
+      if (!x) {
+        free(part);
+        oom(env);
+        return NULL;
+      }
+    } else if (r != d2 || c != d3) {
+      free(part), free(x);
+      iae(env, "Space slabs must all have the same shape");
+      return NULL;
+    }
+    for (size_t k = 0; k < slab; ++k) x[(size_t)i * slab + k] = part[k];
+    free(part);
+  }
+  double* y = malloc(sizeof(double) * (size_t)d1 * (slab ? slab : 1));
+  if (!y) {
+    free(x);
+    oom(env);
+    return NULL;
+  }
+  const jw_fwt_plan* p = (const jw_fwt_plan*)(intptr_t)plan;
+  const int st = op == 0 ? jw_fwt3d_forward(p, x, y, d1, d2, d3, lvlP, lvlQ, lvlR, 1, JW_HOST, NULL)
+                         : jw_fwt3d_reverse(p, x, y, d1, d2, d3, lvlP, lvlQ, lvlR, 1, JW_HOST, NULL);
+  free(x);
+  jobjectArray out = NULL;
+  if (st == JW_OK) {
+    jclass mcls = (*env)->FindClass(env, "[[D");
+    out = mcls ? (*env)->NewObjectArray(env, d1, mcls, NULL) : NULL;
+    for (jsize i = 0; out && i < d1; ++i) {
+      jobjectArray m = rows_out(env, y + (size_t)i * slab, d2, d3);
+      if (!m) {
+        out = NULL;
+        break;
+      }
+      (*env)->SetObjectArrayElement(env, out, i, m);
+      (*env)->DeleteLocalRef(env, m);
+    }
+  }
   free(y);
   if (st != JW_OK) jw_throw(env, st);
   return out;

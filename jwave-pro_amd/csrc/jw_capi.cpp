@@ -236,6 +236,7 @@ struct HostStage {
   double* pin_out[kMaxRing] = {};
   hipEvent_t ev_in[kMaxRing] = {}, ev_out[kMaxRing] = {};  // bounce buffer reuse
   hipEvent_t loaded[2] = {}, done[2] = {}, drained[2] = {};  // sub-batch pipeline
+  hipEvent_t allocated = nullptr;  // the workspaces' stream-ordered allocation, on the caller's stream
 
   ~HostStage() {
     if (dev < 0) return;
@@ -251,6 +252,7 @@ struct HostStage {
     for (int i = 0; i < 2; ++i)
       for (hipEvent_t e : {loaded[i], done[i], drained[i]})
         if (e) (void)hipEventDestroy(e);
+    if (allocated) (void)hipEventDestroy(allocated);
     for (hipStream_t s : {own, h2d, d2h})
       if (s) (void)hipStreamDestroy(s);
   }
@@ -270,6 +272,7 @@ struct HostStage {
     for (int i = 0; i < 2; ++i)
       for (hipEvent_t* e : {&loaded[i], &done[i], &drained[i]})
         JW_HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    JW_HIP_TRY(hipEventCreateWithFlags(&allocated, hipEventDisableTiming));
     return JW_OK;
   }
 
@@ -372,6 +375,11 @@ int run_items(int where, void* stream, const double* in, size_t in_per, double* 
       JW_HIP_TRY(mem.alloc(&din[b], (size_t)sub * in_per * sizeof(double) + 8));
       JW_HIP_TRY(mem.alloc(&dout[b], (size_t)sub * out_per * sizeof(double) + 8));
     }
+    // The pool may hand back blocks whose earlier hipFreeAsync (another call's workspace, or a
+    // JW_DEVICE call queued on the same stream) is ordered only on s: the H2D stream must not
+    // write into them before s reaches this point.
+    JW_HIP_TRY(hipEventRecord(hs->allocated, s));
+    JW_HIP_TRY(hipStreamWaitEvent(hs->h2d, hs->allocated, 0));
     auto count = [&](long k) { return std::min(sub, items - k * sub); };
     auto put = [&](long k) -> int {  // din[k&1] is free once f(k-2) has run
       const int b = (int)(k & 1);
@@ -572,7 +580,10 @@ static bool auto_level_fft(long n, int L, int j, int threshold) {
 //     run the exact-twiddle pyramid (jw_modwt_fft.hip) when any level is FFT.
 //   JW_ARITH_FMA (fast contract): FFT runs the exact-twiddle frequency-domain pyramid; AUTO and
 //     DIRECT run the direct kernels, which are faster and more accurate than any FFT path here.
-enum class ModwtPath { kDirect, kStrictLevels, kPyramid };
+//   A level the reference would run through its FFT at a length neither FFT path takes (n >
+//     2^23) is JW_ERR_UNSUPPORTED with the limit in the message -- never a silent switch to
+//     DIRECT, whose values differ from the JVM's FFT path by up to ~1e-10.
+enum class ModwtPath { kDirect, kStrictLevels, kPyramid, kUnsupported };
 
 static ModwtPath modwt_path(const ModwtPlan& p, int method, long n, int levels, bool* fft) {
   bool any = false;
@@ -582,12 +593,23 @@ static ModwtPath modwt_path(const ModwtPlan& p, int method, long n, int levels, 
     any = any || fft[j];
   }
   if (p.arith == JW_ARITH_FMA) {
-    return method == JW_CONV_FFT && modwt_fft_supported(n) ? ModwtPath::kPyramid
-                                                           : ModwtPath::kDirect;
+    if (method != JW_CONV_FFT) return ModwtPath::kDirect;
+    return modwt_fft_supported(n) ? ModwtPath::kPyramid : ModwtPath::kUnsupported;
   }
   if (!any) return ModwtPath::kDirect;
   if (modwt_strict_fft_supported(n)) return ModwtPath::kStrictLevels;
-  return modwt_fft_supported(n) ? ModwtPath::kPyramid : ModwtPath::kDirect;
+  return modwt_fft_supported(n) ? ModwtPath::kPyramid : ModwtPath::kUnsupported;
+}
+
+static int modwt_unsupported(int method, long n, const bool* fft, int levels) {
+  int j = 1;
+  while (j < levels && !fft[j]) ++j;
+  return fail(JW_ERR_UNSUPPORTED,
+              "MODWT FFT convolution (%s) at signal length %ld: level %d takes the FFT path "
+              "(MODWTTransform.java:640-664) and this engine's FFT convolution supports "
+              "2 <= N <= 2^23 (8388608); use ConvolutionMethod.DIRECT%s",
+              method == JW_CONV_FFT ? "ConvolutionMethod.FFT" : "AUTO", n, j,
+              method == JW_CONV_AUTO ? " or a larger fftConvolutionThreshold" : "");
 }
 
 int jw_modwt_forward(const jw_modwt_plan* plan, const double* x, double* coeffs, long n,
@@ -617,10 +639,12 @@ int jw_modwt_forward(const jw_modwt_plan* plan, const double* x, double* coeffs,
   if (st != JW_OK) return st;
   if (st = check_where(where); st != JW_OK) return st;
   if (!x || !coeffs) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
+  bool fft[kMaxModwtLevel + 1] = {};
+  const ModwtPath path = modwt_path(*plan, method, n, levels, fft);
+  if (path == ModwtPath::kUnsupported) return modwt_unsupported(method, n, fft, levels);
   return run_items(where, stream, x, (size_t)n, coeffs, (size_t)n * (levels + 1), batch,
                    [&](const double* dx, double* dc, long nb, hipStream_t s) {
-                     bool fft[kMaxModwtLevel + 1] = {};
-                     switch (modwt_path(*plan, method, n, levels, fft)) {
+                     switch (path) {
                        case ModwtPath::kStrictLevels:
                          return modwt_forward_strict_device(*plan, dx, dc, n, levels, (int)nb, fft, s);
                        case ModwtPath::kPyramid:
@@ -648,10 +672,12 @@ int jw_modwt_inverse(const jw_modwt_plan* plan, const double* coeffs, double* x,
   if (st != JW_OK) return st;
   if (st = check_where(where); st != JW_OK) return st;
   if (!x || !coeffs) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
+  bool fft[kMaxModwtLevel + 1] = {};
+  const ModwtPath path = modwt_path(*plan, method, n, levels, fft);
+  if (path == ModwtPath::kUnsupported) return modwt_unsupported(method, n, fft, levels);
   return run_items(where, stream, coeffs, (size_t)n * (levels + 1), x, (size_t)n, batch,
                    [&](const double* dc, double* dx, long nb, hipStream_t s) {
-                     bool fft[kMaxModwtLevel + 1] = {};
-                     switch (modwt_path(*plan, method, n, levels, fft)) {
+                     switch (path) {
                        case ModwtPath::kStrictLevels:
                          return modwt_inverse_strict_device(*plan, dc, dx, n, levels, (int)nb, fft, s);
                        case ModwtPath::kPyramid:
@@ -678,8 +704,14 @@ static int fft_call(int S, int arith, const double* in, double* out, long n, int
   if (!in || !out) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
   // STRICT: the reference's own FFT (jw_jfft.hip): radix 2 for powers of two <= 2^24,
   // Bluestein for other n <= 2^23
-  const bool strict = arith == JW_ARITH_STRICT && ((n & (n - 1)) == 0 ? n <= (1L << 24)
-                                                                      : n <= (1L << 23));
+  const bool pow2 = (n & (n - 1)) == 0;
+  const bool strict = arith == JW_ARITH_STRICT;
+  if (strict && n > (pow2 ? (1L << 24) : (1L << 23)))
+    return fail(JW_ERR_UNSUPPORTED,
+                "JW_ARITH_STRICT FFT (FastFourierTransform.java:112-324 operation for operation) "
+                "at length %ld: supported up to 2^24 (16777216) for powers of two and 2^23 "
+                "(8388608) otherwise; JW_ARITH_FMA runs any length",
+                n);
   return run_items(where, stream, in, (size_t)2 * n, out, (size_t)2 * n, batch,
                    [&](const double* di, double* dout, long nb, hipStream_t s) {
                      return strict ? fft_strict_device(S, di, dout, n, nb, s)

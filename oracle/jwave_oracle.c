@@ -6,6 +6,14 @@
  * -O2 -ffp-contract=off (oracle/Makefile): no FMA contraction, left-to-right
  * evaluation exactly as the Java expressions are written.  Every function cites
  * the reference lines it follows (paths relative to src/main/java/jwave/).
+ *
+ * JVM parity of the FFT paths (radix-2 twiddles, Bluestein chirps) rests on one assumption:
+ * Math.sin / Math.cos return the correctly rounded value at every angle those paths take.  Java
+ * specifies them to within 1 ulp only, so a JVM whose intrinsic misrounds an angle would differ
+ * from this oracle (and from the engine, which takes the same correctly rounded values) in that
+ * table entry.  The tests check engine against oracle, which share the assumption; no JVM exists
+ * in this image to generate fixtures that would pin it, so for non-power-of-two lengths (up to
+ * 2^23 chirp angles) "bit-identical to the JVM" means "under correctly rounded sin/cos".
  */
 #include "jwave_oracle.h"
 

@@ -349,3 +349,43 @@ def test_device_ordinal_errors():
 def test_release_caches_without_calls():
     # nothing cached yet in this process (no GPU here): frees nothing, never fails
     assert _native.release_caches() >= 0
+
+
+# ---- no silent method switch past the FFT range (verdict r03: jw_capi.cpp modwt_path) ----
+def test_fft_levels_past_2_23_are_unsupported_not_direct():
+    # JWave runs these levels through its FFT convolution (MODWTTransform.java:640-664,
+    # FastFourierTransform.java:112-164); the engine's FFT paths stop at 2^23, so the call must
+    # fail with the limit named instead of returning DIRECT values (~1e-10 away).
+    lib = _native.lib()
+    n, J = (1 << 23) + 2, 2
+    x = np.zeros(n)
+    c = np.empty((J + 1) * n)
+    vp = ctypes.c_void_p
+    for arith, method in ((_native.JW_ARITH_STRICT, _native.JW_CONV_AUTO),
+                          (_native.JW_ARITH_STRICT, _native.JW_CONV_FFT),
+                          (_native.JW_ARITH_FMA, _native.JW_CONV_FFT)):
+        wv = W.Daubechies4()
+        sd, wd = np.asarray(wv.getScalingDeComposition()), np.asarray(wv.getWaveletDeComposition())
+        plan = vp()
+        assert lib.jw_modwt_plan_create(ctypes.byref(plan), vp(sd.ctypes.data), vp(wd.ctypes.data),
+                                        8, 4096, arith) == _native.JW_OK
+        for fn, a, b in ((lib.jw_modwt_forward, x, c), (lib.jw_modwt_inverse, c, x)):
+            st = fn(plan, vp(a.ctypes.data), vp(b.ctypes.data), n, J, 1, method, _native.JW_HOST, None)
+            assert st == _native.JW_ERR_UNSUPPORTED, (arith, method, st)
+            msg = _native.last_error()
+            assert "2^23" in msg and str(n) in msg and "level 1" in msg, msg
+        lib.jw_modwt_plan_destroy(plan)
+    # the Python mirror raises it (NotImplementedError), never a DIRECT result
+    m = MODWTTransform(W.Daubechies4())
+    with pytest.raises(NotImplementedError, match="2\\^23"):
+        m.forwardMODWT(x, J)
+
+
+def test_strict_fft_past_its_range_is_unsupported():
+    lib = _native.lib()
+    vp = ctypes.c_void_p
+    for n in ((1 << 24) + 2, 1 << 25):
+        z = np.zeros(2 * n)
+        st = lib.jw_fft_forward_ex(vp(z.ctypes.data), vp(z.ctypes.data), n, 1,
+                                   _native.JW_ARITH_STRICT, _native.JW_HOST, None)
+        assert st == _native.JW_ERR_UNSUPPORTED and "2^24" in _native.last_error()

@@ -267,3 +267,24 @@ def test_concurrent_host_threads_with_side_streams():
     finally:
         del os.environ["JW_CWT_OVERLAP"]
     assert np.array_equal(one, alone[0])
+
+
+def test_cfg3_full_scale_set():
+    # BASELINE configs[2] as the bench runs it (64 log scales 2..1024, fs = 1, N = 2^18,
+    # Morlet omega0 = 6), batch 2 through transformFFTBatch (the bench's device path), every
+    # (signal, scale) against the oracle at both bars: normwise over the whole scalogram, and
+    # per scale against that scale's own magnitude
+    n = 1 << 18
+    scales = CWT.generateLogScales(2.0, 1024.0, 64)
+    xs = np.stack([orc.fill_uniform(n, 7 + b) for b in range(2)])
+    import torch
+    got = CWT(MorletWavelet(*MORLET6)).transformFFTBatch(torch.from_numpy(xs).cuda(), scales, 1.0)
+    got = got.cpu().numpy()
+    assert got.shape == (2, 64, n)
+    for b in range(2):
+        ex = orc.cwt_fft(xs[b], scales, 1.0, "morlet", MORLET6, 1, exact=True)
+        jw = orc.cwt_fft(xs[b], scales, 1.0, "morlet", MORLET6, 1, exact=False)
+        assert nw(got[b], ex) < TOL_EXACT, nw(got[b], ex)
+        assert nw(got[b], jw) < TOL_JWAVE, nw(got[b], jw)
+        for i in range(64):
+            assert nw(got[b, i], ex[i]) < 1e-11, (b, i, nw(got[b, i], ex[i]))

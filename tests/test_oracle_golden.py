@@ -146,6 +146,24 @@ def test_haar_filters_vs_fixtures():
     assert np.max(np.abs(np.array(hw.getWaveletDeComposition()) - load_vector("filter_haar_dec_hi.txt"))) < 1e-10
 
 
+def test_haar_reconstruction_filters_vs_fixtures():
+    # testdata/filter_haar_rec_{lo,hi}.txt against Haar1.getScalingReConstruction /
+    # getWaveletReConstruction (Haar1.java:44-70 copies the decomposition filters into the
+    # reconstruction ones), at the reference's 1e-10 (CrossValidationTest.java:158-180).  The
+    # fixture generator writes the high-pass in the time-reversed (pywt) convention,
+    # [-1/sqrt2, 1/sqrt2] (scripts/generate_basic_reference.py:91-92), where JWave keeps
+    # _waveletReCon = _waveletDeCom = [1/sqrt2, -1/sqrt2]: the fixture pins JWave's taps reversed.
+    # No reference test reads these two files; the low-pass is symmetric either way.
+    hw = W.Haar1()
+    lo, hi = load_vector("filter_haar_rec_lo.txt"), load_vector("filter_haar_rec_hi.txt")
+    assert np.max(np.abs(np.array(hw.getScalingReConstruction()) - lo)) < 1e-10
+    assert np.max(np.abs(np.array(hw.getWaveletReConstruction())[::-1] - hi)) < 1e-10
+    assert np.max(np.abs(np.array(hw.getWaveletReConstruction()) - hi)) > 1.0  # not the same order
+    # the reconstruction pair is the decomposition pair (orthonormal), exactly
+    assert np.array_equal(hw.getScalingReConstruction(), hw.getScalingDeComposition())
+    assert np.array_equal(hw.getWaveletReConstruction(), hw.getWaveletDeComposition())
+
+
 def test_daubechies_filters_vs_fixtures():
     # testdata/filter_db2_dec_lo.txt ("Daubechies 2 = Haar", 2 taps) and filter_db4_dec_{lo,hi}.txt
     # (4 taps) use the tap-count naming; JWave names by vanishing moments (DaubechiesK = 2K
