@@ -580,9 +580,10 @@ static bool auto_level_fft(long n, int L, int j, int threshold) {
 //     run the exact-twiddle pyramid (jw_modwt_fft.hip) when any level is FFT.
 //   JW_ARITH_FMA (fast contract): FFT runs the exact-twiddle frequency-domain pyramid; AUTO and
 //     DIRECT run the direct kernels, which are faster and more accurate than any FFT path here.
-//   A level the reference would run through its FFT at a length neither FFT path takes (n >
-//     2^23) is JW_ERR_UNSUPPORTED with the limit in the message -- never a silent switch to
-//     DIRECT, whose values differ from the JVM's FFT path by up to ~1e-10.
+//   A level the reference would run through its FFT at a length the FFT paths do not take
+//     (STRICT: powers of two past 2^28, other n past 2^23; FMA's pyramid: n past 2^23) is
+//     JW_ERR_UNSUPPORTED with the limit in the message -- never a silent switch to DIRECT, whose
+//     values differ from the JVM's FFT path by up to ~1e-10.
 enum class ModwtPath { kDirect, kStrictLevels, kPyramid, kUnsupported };
 
 static ModwtPath modwt_path(const ModwtPlan& p, int method, long n, int levels, bool* fft) {
@@ -601,14 +602,18 @@ static ModwtPath modwt_path(const ModwtPlan& p, int method, long n, int levels, 
   return modwt_fft_supported(n) ? ModwtPath::kPyramid : ModwtPath::kUnsupported;
 }
 
-static int modwt_unsupported(int method, long n, const bool* fft, int levels) {
+static int modwt_unsupported(int arith, int method, long n, const bool* fft, int levels) {
   int j = 1;
   while (j < levels && !fft[j]) ++j;
   return fail(JW_ERR_UNSUPPORTED,
               "MODWT FFT convolution (%s) at signal length %ld: level %d takes the FFT path "
-              "(MODWTTransform.java:640-664) and this engine's FFT convolution supports "
-              "2 <= N <= 2^23 (8388608); use ConvolutionMethod.DIRECT%s",
+              "(MODWTTransform.java:640-664) and this engine's %s FFT convolution supports %s; "
+              "use ConvolutionMethod.DIRECT%s",
               method == JW_CONV_FFT ? "ConvolutionMethod.FFT" : "AUTO", n, j,
+              arith == JW_ARITH_STRICT ? "STRICT" : "FMA",
+              arith == JW_ARITH_STRICT
+                  ? "powers of two up to 2^28 (268435456) and other lengths up to 2^23 (8388608)"
+                  : "2 <= N <= 2^23 (8388608)",
               method == JW_CONV_AUTO ? " or a larger fftConvolutionThreshold" : "");
 }
 
@@ -641,7 +646,7 @@ int jw_modwt_forward(const jw_modwt_plan* plan, const double* x, double* coeffs,
   if (!x || !coeffs) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
   bool fft[kMaxModwtLevel + 1] = {};
   const ModwtPath path = modwt_path(*plan, method, n, levels, fft);
-  if (path == ModwtPath::kUnsupported) return modwt_unsupported(method, n, fft, levels);
+  if (path == ModwtPath::kUnsupported) return modwt_unsupported(plan->arith, method, n, fft, levels);
   return run_items(where, stream, x, (size_t)n, coeffs, (size_t)n * (levels + 1), batch,
                    [&](const double* dx, double* dc, long nb, hipStream_t s) {
                      switch (path) {
@@ -674,7 +679,7 @@ int jw_modwt_inverse(const jw_modwt_plan* plan, const double* coeffs, double* x,
   if (!x || !coeffs) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
   bool fft[kMaxModwtLevel + 1] = {};
   const ModwtPath path = modwt_path(*plan, method, n, levels, fft);
-  if (path == ModwtPath::kUnsupported) return modwt_unsupported(method, n, fft, levels);
+  if (path == ModwtPath::kUnsupported) return modwt_unsupported(plan->arith, method, n, fft, levels);
   return run_items(where, stream, coeffs, (size_t)n * (levels + 1), x, (size_t)n, batch,
                    [&](const double* dc, double* dx, long nb, hipStream_t s) {
                      switch (path) {
@@ -706,10 +711,10 @@ static int fft_call(int S, int arith, const double* in, double* out, long n, int
   // Bluestein for other n <= 2^23
   const bool pow2 = (n & (n - 1)) == 0;
   const bool strict = arith == JW_ARITH_STRICT;
-  if (strict && n > (pow2 ? (1L << 24) : (1L << 23)))
+  if (strict && n > (pow2 ? (1L << 28) : (1L << 23)))
     return fail(JW_ERR_UNSUPPORTED,
                 "JW_ARITH_STRICT FFT (FastFourierTransform.java:112-324 operation for operation) "
-                "at length %ld: supported up to 2^24 (16777216) for powers of two and 2^23 "
+                "at length %ld: supported up to 2^28 (268435456) for powers of two and 2^23 "
                 "(8388608) otherwise; JW_ARITH_FMA runs any length",
                 n);
   return run_items(where, stream, in, (size_t)2 * n, out, (size_t)2 * n, batch,

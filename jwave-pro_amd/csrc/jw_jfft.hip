@@ -6,6 +6,7 @@
 // so a default-constructed MODWTTransform (AUTO) gets the JVM's values bit for bit.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -74,6 +75,50 @@ int twiddles(long n, bool inverse, int lc1, Tw* out, StreamAllocs& mem, hipStrea
   out->lc1 = one ? (int)n : lc1;
   out->p1 = (const cplx*)p;
   out->p2 = one ? nullptr : (const cplx*)p + lc1;
+  return JW_OK;
+}
+
+long three_pass_min() {
+  const char* e = std::getenv("JW_JFFT_3PASS_MIN");  // tests: a power of two >= 2^18
+  long m = e ? std::atol(e) : 0;
+  if (m < (1L << 18) || (m & (m - 1))) m = 1L << 25;
+  return m;
+}
+
+using Tw3Key = std::tuple<int, long, int>;  // device, n, inverse (the split is a function of n)
+DevCache<Tw3Key> g_tw3(kCacheBytes);
+
+int twiddles3(long n, bool inverse, Tw3* out, StreamAllocs& mem, hipStream_t s) {
+  int dev = 0;
+  JW_HIP_TRY(hipGetDevice(&dev));
+  int a, b, c;
+  split3(ilog2(n), &a, &b, &c);
+  const long A = 1L << a, B = 1L << b, C = 1L << c, AB = A * B;
+  const size_t entries = (size_t)(A + AB + n);
+  const void* p = nullptr;
+  int st = cached_table(g_tw3, Tw3Key(dev, n, inverse ? 1 : 0), entries * sizeof(cplx), mem, s, &p,
+                        [&](void* d) -> int {
+                          std::vector<cplx> tw;
+                          java_twiddles(n, inverse, tw);
+                          std::vector<cplx> h(entries);
+                          std::copy(tw.begin(), tw.begin() + A, h.begin());
+                          cplx* pm = h.data() + A;
+                          for (long l = 0; l < A; ++l)
+                            for (long m = 0; m < B; ++m) pm[l * B + m] = tw[m * A + l];
+                          cplx* p3 = pm + AB;
+                          for (long l = 0; l < AB; ++l)
+                            for (long m = 0; m < C; ++m) p3[l * C + m] = tw[m * AB + l];
+                          JW_HIP_TRY(upload_async(d, h.data(), entries * sizeof(cplx), s));
+                          return JW_OK;
+                        });
+  if (st != JW_OK) return st;
+  out->n = n;
+  out->A = (int)A;
+  out->B = (int)B;
+  out->C = (int)C;
+  out->p1 = (const cplx*)p;
+  out->pm = out->p1 + A;
+  out->p3 = out->pm + AB;
   return JW_OK;
 }
 
@@ -317,6 +362,87 @@ int inverse_cols(const ModwtPlan& p, const bool* fft, const cplx* F, const Tw& t
   return st;
 }
 
+// P[i] = X[i].mul(F[i]) (circularConvolveFFT :775-778), or with F[i].conjugate() (:820-824)
+template <bool CONJ>
+__global__ __launch_bounds__(256) void kmul_spec(const cplx* __restrict__ X,
+                                                 const cplx* __restrict__ F, cplx* __restrict__ P,
+                                                 long n) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const cplx f = F[i];
+    P[i] = jmul(X[i], CONJ ? make_double2(f.x, -f.y) : f);
+  }
+}
+
+template <bool CONJ>
+int mul_spec(const cplx* X, const cplx* F, cplx* P, long n, hipStream_t s) {
+  const long blocks = std::min<long>((n + 255) / 256, 65536);
+  hipLaunchKernelGGL(kmul_spec<CONJ>, dim3((unsigned)blocks), dim3(256), 0, s, X, F, P, n);
+  JW_HIP_TRY(hipGetLastError());
+  return JW_OK;
+}
+
+// Long lines (three-pass transforms): each FFT level exactly as the reference writes it, one
+// signal and one transform at a time -- FFT(V) (Complex(v, 0)), the product with the level's
+// filter spectrum, the reverse FFT with its 1/n, the real part (:752-837); DIRECT levels
+// through the direct per-level kernels.  Unfused (these lengths are for parity, not speed).
+int modwt_strict_long(bool inverse, const ModwtPlan& p, const double* in, double* out, long N,
+                      int J, int batch, const bool* fft, const cplx* F, StreamAllocs& mem,
+                      hipStream_t s) {
+  const long rs = (long)(J + 1) * N;
+  cplx *X = nullptr, *P = nullptr;
+  double* tmp = nullptr;
+  JW_HIP_TRY(mem.alloc(&X, (size_t)N * sizeof(cplx)));
+  JW_HIP_TRY(mem.alloc(&P, (size_t)N * sizeof(cplx)));
+  JW_HIP_TRY(mem.alloc(&tmp, (size_t)2 * N * sizeof(double)));
+  const double inv_n = 1.0 / (double)N;
+  int st = JW_OK;
+  auto fwd = [&](const double* v) {  // X = FFT(Complex(v, 0))
+    return fft_rows(N, false, 1, RowsR{v, N}, OutCS{X, N, 1.0, 0}, mem, s);
+  };
+  for (long b = 0; b < batch && st == JW_OK; ++b) {
+    if (!inverse) {
+      const double* x = in + b * N;
+      double* c = out + b * rs;
+      const double* vin = x;
+      for (int j = 1; j <= J && st == JW_OK; ++j) {
+        double* w = c + (long)(j - 1) * N;
+        double* vout = j == J ? c + (long)J * N : tmp + (long)(j & 1) * N;
+        if (!fft[j]) {
+          st = modwt_level_forward_device(p, j, vin, N, w, rs, vout, N, N, 1, s);
+        } else if ((st = fwd(vin)) == JW_OK &&
+                   (st = mul_spec<false>(X, spec_h(F, N, j), P, N, s)) == JW_OK &&
+                   (st = fft_rows(N, true, 1, RowsC{P, N}, OutRe<false>{w, N, inv_n}, mem, s)) ==
+                       JW_OK &&
+                   (st = mul_spec<false>(X, spec_g(F, N, j), P, N, s)) == JW_OK) {
+          st = fft_rows(N, true, 1, RowsC{P, N}, OutRe<false>{vout, N, inv_n}, mem, s);
+        }
+        vin = vout;
+      }
+    } else {
+      const double* c = in + b * rs;
+      double* x = out + b * N;
+      const double* vin = c + (long)J * N;
+      for (int j = J; j >= 1 && st == JW_OK; --j) {
+        const double* w = c + (long)(j - 1) * N;
+        double* vout = j == 1 ? x : tmp + (long)(j & 1) * N;
+        if (!fft[j]) {
+          st = modwt_level_inverse_device(p, j, vin, N, w, rs, vout, N, N, 1, s);
+        } else if ((st = fwd(vin)) == JW_OK &&
+                   (st = mul_spec<true>(X, spec_g(F, N, j), P, N, s)) == JW_OK &&
+                   (st = fft_rows(N, true, 1, RowsC{P, N}, OutRe<false>{vout, N, inv_n}, mem,
+                                  s)) == JW_OK &&
+                   (st = fwd(w)) == JW_OK &&
+                   (st = mul_spec<true>(X, spec_h(F, N, j), P, N, s)) == JW_OK) {
+          // vFromApprox[i] + vFromDetail[i] (:366-369)
+          st = fft_rows(N, true, 1, RowsC{P, N}, OutRe<true>{vout, N, inv_n}, mem, s);
+        }
+        vin = vout;
+      }
+    }
+  }
+  return st;
+}
+
 int modwt_strict(bool inverse, const ModwtPlan& p, const double* in, double* out, long N, int J,
                  int batch, const bool* fft, hipStream_t s) {
   StreamAllocs mem(s);
@@ -324,6 +450,8 @@ int modwt_strict(bool inverse, const ModwtPlan& p, const double* in, double* out
   int st = filter_spectra(p, N, J, &F, mem, s);
   if (st != JW_OK) return st;
   if (N & (N - 1)) return modwt_strict_bs(inverse, p, in, out, N, J, batch, fft, F, mem, s);
+  if (N > kLineMax && N >= three_pass_min())
+    return modwt_strict_long(inverse, p, in, out, N, J, batch, fft, F, mem, s);
   const long rs = (long)(J + 1) * N;
   if (N <= kLineMax) {
     Tw twf, twi;
@@ -372,9 +500,11 @@ int modwt_strict(bool inverse, const ModwtPlan& p, const double* in, double* out
 // ---------------------------------------------------------------------------------------
 // entry points (jw_internal.hpp)
 // ---------------------------------------------------------------------------------------
-// every length the reference's FFT path takes here: powers of two (radix 2) and, through
-// Bluestein with m <= 2^24, any other n <= 2^23
-bool modwt_strict_fft_supported(long n) { return n >= 2 && n <= (1L << 23); }
+// every length the reference's FFT path takes here: powers of two (radix 2) up to 2^28 and,
+// through Bluestein with m <= 2^24, any other n <= 2^23
+bool modwt_strict_fft_supported(long n) {
+  return n >= 2 && ((n & (n - 1)) == 0 ? n <= jf::kStrictPow2Max : n <= (1L << 23));
+}
 
 int modwt_forward_strict_device(const ModwtPlan& p, const double* x, double* coeffs, long n,
                                 int J, int batch, const bool* fft_level, hipStream_t s) {
@@ -398,7 +528,8 @@ int fft_strict_device(int S, const double* in, double* out, long n, long batch, 
     if (n > (1L << 23)) return fail(JW_ERR_UNSUPPORTED, "Java-order FFT: length %ld > 2^23", n);
     return jf::bs_fft_strict(S > 0, (const jf::cplx*)in, (jf::cplx*)out, n, batch, s);
   }
-  if (n > (1L << 24)) return fail(JW_ERR_UNSUPPORTED, "Java-order FFT: length %ld > 2^24", n);
+  if (n > jf::kStrictPow2Max)
+    return fail(JW_ERR_UNSUPPORTED, "Java-order FFT: length %ld > 2^28", n);
   // in == out is safe: a line is read whole before it is written, and the column path reads
   // the input in pass 1 and writes the output in pass 2 (from the workspace Z)
   StreamAllocs mem(s);

@@ -23,9 +23,35 @@ struct Tw {
 // pass-1 length of an n-point transform (n itself when it runs in one column)
 inline int split_lc1(long n) { return n <= kLineMax ? (int)n : 1 << (ilog2(n) / 2); }
 
+// Power-of-two transforms from here on run as three column passes (n = A x B x C, each a
+// column of 64 .. 4096 points): the two-pass split stops at 4096 x 4096 = 2^24.  2^25 by
+// default; env JW_JFFT_3PASS_MIN (a power of two >= 2^18) lowers it, so the tests can check the
+// three-pass code against the oracle at sizes the oracle finishes quickly.
+long three_pass_min();
+constexpr long kStrictPow2Max = 1L << 28;  // the longest power-of-two STRICT transform
+// bits of A, B, C for a three-pass n = 2^lg (18 <= lg <= 36)
+inline void split3(int lg, int* a, int* b, int* c) {
+  *a = std::min(12, lg - 12);
+  const int rem = lg - *a;
+  *b = std::max(6, rem - 12);
+  *c = rem - *b;
+}
+
 // Twiddles of an n-point transform in the reference's recurrence order, laid out for a split
 // with pass-1 length lc1 (jw_jfft.hip); cached per (device, n, direction, lc1).
 int twiddles(long n, bool inverse, int lc1, Tw* out, StreamAllocs& mem, hipStream_t s);
+
+// Twiddles of a three-pass transform: p1 = Tw[0 .. A) (pass 1, natural), pm[l B + m] =
+// Tw[m A + l] (pass 2 over planes of [B][A], l < A, m < B), p3[l C + m] = Tw[m A B + l] (pass 3,
+// l < A B, m < C); Tw in the reference's recurrence order.
+struct Tw3 {
+  long n = 0;
+  int A = 0, B = 0, C = 0;
+  const cplx* p1 = nullptr;
+  const cplx* pm = nullptr;
+  const cplx* p3 = nullptr;
+};
+int twiddles3(long n, bool inverse, Tw3* out, StreamAllocs& mem, hipStream_t s);
 
 // ---------------------------------------------------------------------------------------
 // Launch helpers: runtime column length -> template instantiation
@@ -97,6 +123,36 @@ struct OutR {
   double* p;
   long st;
   __device__ void operator()(long it, long i, double v) const { p[it * st + i] = v; }
+};
+// result[i].mul(1.0 / n).getReal() of a reverse transform (:207-211, :781-783) into a real row;
+// ADD: added to the value already there (vFromApprox[i] + vFromDetail[i], :366-369)
+template <bool ADD>
+struct OutRe {
+  double* p;
+  long st;
+  double sc;
+  __device__ void operator()(long it, long i, cplx v) const {
+    const double r = v.x * sc;
+    if constexpr (ADD) {
+      p[it * st + i] = p[it * st + i] + r;
+    } else {
+      p[it * st + i] = r;
+    }
+  }
+};
+// the middle pass of a three-pass transform: item it' = item * C + plane o, natural index
+// i = h A + l of the plane's [B][A] view at o A B + i of the item's n points (read and written
+// in place: a workgroup writes exactly the points it read)
+struct Plane {
+  cplx* p;
+  long n, ab;
+  int cbits;
+  __device__ cplx operator()(long it, long i) const {
+    return p[(it >> cbits) * n + (it & ((1L << cbits) - 1)) * ab + i];
+  }
+  __device__ void operator()(long it, long i, cplx v) const {
+    p[(it >> cbits) * n + (it & ((1L << cbits) - 1)) * ab + i] = v;
+  }
 };
 // NF row outputs, stream f at p + f * fst
 struct OutF {
@@ -188,9 +244,55 @@ struct LineAdjMid {  // s = 0: V_j with g_j, s = 1: W_j with h_j
 // ---------------------------------------------------------------------------------------
 // Natural-order transforms of `items` rows: in (RowsR / RowsC) -> out (OutCS)
 // ---------------------------------------------------------------------------------------
-template <class In>
-inline int fft_rows(long n, bool inverse, long items, In in, OutCS out, StreamAllocs& mem,
+// Three column passes (n >= three_pass_min()): pass 1 = the first log A stages on the
+// bit-reversed blocks of A points (kp1, rows of Z), pass 2 = the next log B stages on columns of
+// stride A within each plane of A B points (kp2s in place), pass 3 = the last log C stages on
+// columns of stride A B (kp2s into Out).  Same butterflies, same twiddles, same order as the
+// two-pass split: stage t pairs positions p, p + 2^t with Tw[2^t + p mod 2^t] whatever the
+// pass boundaries (jw_jfft.hpp).
+template <class In, class Out>
+inline int fft_rows3(long n, bool inverse, long items, In in, Out out, StreamAllocs& mem,
+                     hipStream_t s) {
+  Tw3 tw;
+  int st = twiddles3(n, inverse, &tw, mem, s);
+  if (st != JW_OK) return st;
+  const int abits = ilog2(tw.A), cbits = ilog2(tw.C);
+  const long ab = (long)tw.A * tw.B;
+  const long chunk = std::max(1L, std::min<long>(items, (1L << 30) / (n * (long)sizeof(cplx))));
+  cplx* Z = nullptr;
+  JW_HIP_TRY(mem.alloc(&Z, (size_t)chunk * n * sizeof(cplx)));
+  for (long i0 = 0; i0 < items && st == JW_OK; i0 += chunk) {
+    const long ni = std::min(chunk, items - i0);
+    In in_c = in;
+    in_c.p += i0 * in.st;
+    Out out_c = out;
+    out_c.p += i0 * out.st;
+    st = with_big_lc(tw.A, [&](auto LCc) -> int {
+      constexpr int LC = decltype(LCc)::value;
+      return launch_grid<LC>(kp1<LC, In, OutC>, (n / tw.A / Geo<LC>::T) * ni, s, in_c,
+                             OutC{Z, n}, ilog2(n / tw.A), ni, tw.p1);
+    });
+    if (st != JW_OK) break;
+    st = with_big_lc(tw.B, [&](auto LCc) -> int {
+      constexpr int LC = decltype(LCc)::value;
+      const Plane pl{Z, n, ab, cbits};
+      return launch_grid<LC>(kp2s<LC, Plane, Plane>, (tw.A / Geo<LC>::T) * ni * tw.C, s, pl, pl,
+                             abits, ni * tw.C, tw.pm);
+    });
+    if (st != JW_OK) break;
+    st = with_big_lc(tw.C, [&](auto LCc) -> int {
+      constexpr int LC = decltype(LCc)::value;
+      return launch_grid<LC>(kp2s<LC, RowsC, Out>, (ab / Geo<LC>::T) * ni, s, RowsC{Z, n}, out_c,
+                             ilog2(ab), ni, tw.p3);
+    });
+  }
+  return st;
+}
+
+template <class In, class Out = OutCS>
+inline int fft_rows(long n, bool inverse, long items, In in, Out out, StreamAllocs& mem,
              hipStream_t s) {
+  if (n > kLineMax && n >= three_pass_min()) return fft_rows3(n, inverse, items, in, out, mem, s);
   const int lc1 = split_lc1(n);
   Tw tw;
   int st = twiddles(n, inverse, lc1, &tw, mem, s);
@@ -198,7 +300,7 @@ inline int fft_rows(long n, bool inverse, long items, In in, OutCS out, StreamAl
   if (n <= kLineMax) {
     return with_lc(n, [&](auto LCc) -> int {
       constexpr int LC = decltype(LCc)::value;
-      return launch_grid<LC>(kline_fft<LC, In, OutCS>, (items + Geo<LC>::T - 1) / Geo<LC>::T, s,
+      return launch_grid<LC>(kline_fft<LC, In, Out>, (items + Geo<LC>::T - 1) / Geo<LC>::T, s,
                              in, out, items, tw.p1, 1.0, 0);
     });
   }
@@ -210,7 +312,7 @@ inline int fft_rows(long n, bool inverse, long items, In in, OutCS out, StreamAl
     const long ni = std::min(chunk, items - i0);
     In in_c = in;
     in_c.p += i0 * in.st;
-    OutCS out_c = out;
+    Out out_c = out;
     out_c.p += i0 * out.st;
     st = with_big_lc(lc1, [&](auto LCc) -> int {
       constexpr int LC = decltype(LCc)::value;
@@ -220,7 +322,7 @@ inline int fft_rows(long n, bool inverse, long items, In in, OutCS out, StreamAl
     if (st != JW_OK) break;
     st = with_big_lc(lc2, [&](auto LCc) -> int {
       constexpr int LC = decltype(LCc)::value;
-      return launch_grid<LC>(kp2s<LC, RowsC, OutCS>, (lc1 / Geo<LC>::T) * ni, s, RowsC{Z, n},
+      return launch_grid<LC>(kp2s<LC, RowsC, Out>, (lc1 / Geo<LC>::T) * ni, s, RowsC{Z, n},
                              out_c, ilog2(lc1), ni, tw.p2);
     });
   }

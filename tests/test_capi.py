@@ -382,10 +382,13 @@ def test_fft_levels_past_2_23_are_unsupported_not_direct():
 
 
 def test_strict_fft_past_its_range_is_unsupported():
+    # STRICT runs the reference's FFT for powers of two up to 2^28 (three column passes past
+    # 2^24) and Bluestein up to 2^23; past those, an error naming the limits
     lib = _native.lib()
     vp = ctypes.c_void_p
-    for n in ((1 << 24) + 2, 1 << 25):
-        z = np.zeros(2 * n)
+    for n in ((1 << 23) + 2, 1 << 29):
+        z = np.zeros(2 * n)  # calloc: pages untouched
         st = lib.jw_fft_forward_ex(vp(z.ctypes.data), vp(z.ctypes.data), n, 1,
                                    _native.JW_ARITH_STRICT, _native.JW_HOST, None)
-        assert st == _native.JW_ERR_UNSUPPORTED and "2^24" in _native.last_error()
+        msg = _native.last_error()
+        assert st == _native.JW_ERR_UNSUPPORTED and "2^28" in msg and "2^23" in msg, msg

@@ -209,3 +209,55 @@ def test_fft_method_bluestein_bit_exact(wname, n, J):
     c = m.forwardMODWT(x, J)
     assert bits_equal(c, orc.modwt_forward(x, J, g, h, "fft"))
     assert bits_equal(m.inverseMODWT(c), orc.modwt_inverse(c, g, h, "fft"))
+
+
+# ---- three column passes (powers of two past 2^24, up to 2^28) ----
+# JW_JFFT_3PASS_MIN lowers the length where the three-pass transform (jw_jfft_host.hpp
+# fft_rows3) and the unfused long-line MODWT (jw_jfft.hip modwt_strict_long) take over, so they
+# are checked against the oracle at lengths it finishes in seconds; one real 2^25 transform too.
+@pytest.mark.parametrize("n", [1 << 18, 1 << 19, 1 << 20, 1 << 22])
+def test_fft_strict_three_pass_bit_exact(n, monkeypatch):
+    monkeypatch.setenv("JW_JFFT_3PASS_MIN", str(1 << 18))
+    rng = np.random.default_rng(n + 3)
+    B = 2 if n <= (1 << 20) else 1
+    z = rng.uniform(-1, 1, (B, n)) + 1j * rng.uniform(-1, 1, (B, n))
+    f = FastFourierTransform()
+    X = f.forwardComplex(z)
+    for b in range(B):
+        assert bits_equal(X[b].view(np.float64), orc.fft(z[b]).view(np.float64)), b
+    zr = f.reverseComplex(X)
+    for b in range(B):
+        assert bits_equal(zr[b].view(np.float64), orc.fft(X[b], inverse=True).view(np.float64)), b
+
+
+# (wavelet, n, J, threshold, method): all-FFT, mixed DIRECT/FFT levels (a threshold that keeps
+# the short filters DIRECT), the int32 wrap (db4 level 12 at 2^18: N M_12 >= 2^31 -> DIRECT)
+LONG_CASES = [("Daubechies4", 1 << 18, 4, 4096, "auto"), ("Symlet8", 1 << 19, 3, 4096, "fft"),
+              ("Daubechies4", 1 << 18, 7, (1 << 18) * 100, "auto"),
+              ("Daubechies4", 1 << 18, 12, 4096, "auto"), ("Haar1", 1 << 20, 2, 4096, "auto")]
+
+
+@pytest.mark.parametrize("wname,n,J,threshold,method", LONG_CASES)
+def test_modwt_long_lines_bit_exact(wname, n, J, threshold, method, monkeypatch):
+    monkeypatch.setenv("JW_JFFT_3PASS_MIN", str(1 << 18))
+    wv = W.by_name(wname)
+    g, h = ofilters(wv)
+    xs = np.stack([orc.fill_uniform(n, 5 + b) for b in range(2)])
+    m = MODWTTransform(wv, fftThreshold=threshold)
+    if method == "fft":
+        m.setConvolutionMethod(ConvolutionMethod.FFT)
+    c = m.forwardMODWT(xs, J)
+    xr = m.inverseMODWT(c)
+    for b in range(2):
+        ref = orc.modwt_forward(xs[b], J, g, h, method, threshold)
+        assert bits_equal(c[b], ref), b
+        assert bits_equal(xr[b], orc.modwt_inverse(ref, g, h, method, threshold)), b
+
+
+def test_fft_strict_2_25():
+    # the smallest length past the two-pass split, with the default (three-pass) geometry
+    n = 1 << 25
+    rng = np.random.default_rng(25)
+    z = rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n)
+    X = FastFourierTransform().forwardComplex(z)
+    assert bits_equal(X.view(np.float64), orc.fft(z).view(np.float64))
