@@ -522,7 +522,46 @@ def main():
                 f"MISMATCH max {float(np.max(np.abs(got - ref)))}"
         return f"normwise {float(np.max(np.abs(got - ref)) / np.max(np.abs(ref))):.2e}"
 
-    def extra_paths(nb=16, reps=3):
+    def auto_strict_bytes(nsig, L, threshold=4096):
+        """HBM bytes one jw_modwt_forward + jw_modwt_inverse of JWave's default path (AUTO,
+        JW_ARITH_STRICT) must move with the engine's kernel structure (jw_jfft.hip
+        forward_cols / inverse_cols, power-of-two n > 4096): every kernel reads its inputs and
+        writes its outputs once.  Per FFT level, forward: [kp1 of V_{j-1}: 8n in, 16n out, unless
+        the previous level fused it] + kp2p (two items: 2 x 16n in, 2 x 16n out) + kp2r for W_j
+        (16n in, 8n out) + kp2r for V_j (16n in; 16n out fused into the next FFT level's pass 1,
+        else 8n); inverse: [kp1 of V_j unless fused] + kp1 of W_j (8n in, 16n out) + kp2p (2 x 16n
+        in and out) + kp2r of both (2 x 16n in; 16n out fused, else 8n).  DIRECT levels: the
+        per-level direct kernels (forward 8n in, 16n out; inverse 16n in, 8n out)."""
+        import numpy as np  # noqa: F401
+        if n <= 4096 or n & (n - 1):
+            return None
+        def fft_level(j):  # MODWTTransform.java:653, int32 product
+            m = (L - 1) * (1 << (j - 1)) + 1
+            prod = (n * m) & 0xffffffff
+            prod = prod - (1 << 32) if prod >= (1 << 31) else prod
+            return prod > threshold
+        f = [None] + [fft_level(j) for j in range(1, J + 1)]
+        total, fused = 0, False
+        for j in range(1, J + 1):  # forward
+            if not f[j]:
+                total += 24 * n
+                fused = False
+                continue
+            nxt = j < J and f[j + 1]
+            total += (0 if fused else 24 * n) + 64 * n + 24 * n + (32 if nxt else 24) * n
+            fused = nxt
+        fused = False
+        for j in range(J, 0, -1):  # inverse
+            if not f[j]:
+                total += 24 * n
+                fused = False
+                continue
+            nxt = j > 1 and f[j - 1]
+            total += (0 if fused else 24 * n) + 24 * n + 64 * n + (48 if nxt else 40) * n
+            fused = nxt
+        return total * nsig
+
+    def extra_paths(nb=16, reps=3, nb_auto=128):
         """Secondary figures on a 16-signal sub-batch (never the headline):
         * JW_HOST: host double[] in, host double[] out -- what a JNI caller passing Java arrays
           gets, PCIe staging included;
@@ -577,6 +616,7 @@ def main():
                               "ms_per_call_pair": round(t1 * 1e3, 3),
                               "note": "batch 1 per call (the reference API's unit; JNI nForward + "
                                       "nInverse), host arrays, PCIe staging included"}
+        nb = min(nb_auto, Bl)  # AUTO / FFT legs: a batch that fills the chip
         ca = torch.empty((nb, J + 1, n), dtype=torch.float64, device=dev)
         xra = torch.empty((nb, n), dtype=torch.float64, device=dev)
 
@@ -613,6 +653,16 @@ def main():
                 "max_abs_vs_reference_path": float(np.max(np.abs(got - jw_auto))),
                 "reference_path_vs_exact_direct": dev_rows(jw_auto, exact),
                 "recon_max_abs": (xra - x[:nb]).abs().max().item()}
+        ab = auto_strict_bytes(nb, len(wv.getScalingDeComposition()))
+        if ab:
+            auto["roofline"] = {
+                "bound": "hbm", "achieved": round(ab / ta / 1e9, 1), "peak": 8000.0,
+                "unit": "GB/s", "frac": round(ab / ta / 8e12, 4),
+                "bytes_per_sample": ab / (nb * n),
+                "note": "bytes = what the AUTO STRICT kernel chain must move, every kernel reading "
+                        "its inputs and writing its outputs once (bench.py auto_strict_bytes: the "
+                        "three FFT-sized complex transforms per forward level, four per inverse "
+                        "level, each two column passes through HBM) / forward+inverse time"}
         tp = timed("fma", _native.JW_CONV_FFT)
         got = ca[0].cpu().numpy()
         auto["fft_pyramid_fma"] = {

@@ -16,10 +16,10 @@
 
 typedef double d2v __attribute__((ext_vector_type(2)));
 
-template <int RIN, int ROUT, int U, bool REV, int ORDER>
-__global__ __launch_bounds__(256) void rows(const double* __restrict__ in, double* __restrict__ out,
-                                            long N, long seg) {
-  constexpr int C = 512;
+template <int RIN, int ROUT, int U, bool REV, int ORDER, int NT = 256>
+__global__ __launch_bounds__(NT) void rows(const double* __restrict__ in, double* __restrict__ out,
+                                           long N, long seg) {
+  constexpr int C = 2 * NT;
   const int t = threadIdx.x;
   const double* ib = in + (long)blockIdx.y * RIN * N;
   double* ob = out + (long)blockIdx.y * ROUT * N;
@@ -105,5 +105,19 @@ int main() {
   shapes<4, 0>(ri, ro, N, B, "step-major");
   shapes<4, 1>(ri, ro, N, B, "row-major ");
   shapes<8, 1>(ri, ro, N, B, "row-major ");
+  // one wave per segment (the inverse wave kernels' shape: 1 KB per row per step)
+  {
+    const double bytes = 80.0 * N * B;
+    for (long seg : {131072L, 16384L}) {
+      dim3 g((unsigned)(N / seg), (unsigned)B);
+      char nm[96];
+      snprintf(nm, 96, "9->1 wave U=2 step-major seg=%ld", seg);
+      timeit(nm, [&] { rows<9, 1, 2, true, 0, 64><<<g, 64>>>(ri, ro, N, seg); }, bytes);
+      snprintf(nm, 96, "9->1 wave U=4 row-major seg=%ld", seg);
+      timeit(nm, [&] { rows<9, 1, 4, true, 1, 64><<<g, 64>>>(ri, ro, N, seg); }, bytes);
+      snprintf(nm, 96, "9->1 wave U=8 row-major seg=%ld", seg);
+      timeit(nm, [&] { rows<9, 1, 8, true, 1, 64><<<g, 64>>>(ri, ro, N, seg); }, bytes);
+    }
+  }
   return 0;
 }
