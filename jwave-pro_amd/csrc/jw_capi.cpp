@@ -612,7 +612,7 @@ static int modwt_unsupported(int arith, int method, long n, const bool* fft, int
               method == JW_CONV_FFT ? "ConvolutionMethod.FFT" : "AUTO", n, j,
               arith == JW_ARITH_STRICT ? "STRICT" : "FMA",
               arith == JW_ARITH_STRICT
-                  ? "powers of two up to 2^28 (268435456) and other lengths up to 2^23 (8388608)"
+                  ? "powers of two up to 2^28 (268435456) and other lengths up to 2^27 (134217728)"
                   : "2 <= N <= 2^23 (8388608)",
               method == JW_CONV_AUTO ? " or a larger fftConvolutionThreshold" : "");
 }
@@ -711,11 +711,11 @@ static int fft_call(int S, int arith, const double* in, double* out, long n, int
   // Bluestein for other n <= 2^23
   const bool pow2 = (n & (n - 1)) == 0;
   const bool strict = arith == JW_ARITH_STRICT;
-  if (strict && n > (pow2 ? (1L << 28) : (1L << 23)))
+  if (strict && n > (pow2 ? (1L << 28) : (1L << 27)))
     return fail(JW_ERR_UNSUPPORTED,
                 "JW_ARITH_STRICT FFT (FastFourierTransform.java:112-324 operation for operation) "
-                "at length %ld: supported up to 2^28 (268435456) for powers of two and 2^23 "
-                "(8388608) otherwise; JW_ARITH_FMA runs any length",
+                "at length %ld: supported up to 2^28 (268435456) for powers of two and 2^27 "
+                "(134217728) otherwise (Bluestein's m <= 2^28); JW_ARITH_FMA runs any length",
                 n);
   return run_items(where, stream, in, (size_t)2 * n, out, (size_t)2 * n, batch,
                    [&](const double* di, double* dout, long nb, hipStream_t s) {

@@ -43,11 +43,18 @@ __host__ __device__ constexpr int ilog2(long v) {
   return r;
 }
 
+// A/B builds (tools/build_variant.sh): points per thread of the 1024-point columns.  16 makes
+// a 1024-point column one wavefront (wave-level syncs, radix-16 register groups, 8 columns =
+// 128-byte pieces per workgroup) at 139 KB of LDS, one workgroup per CU.
+#ifndef JF_EPT1024
+#define JF_EPT1024 8
+#endif
 template <int LC>
 struct Geo {
   static constexpr int LOG = ilog2(LC);
   // (a 4096-point column needs 16 per thread: at most kNT threads per column)
-  static constexpr int EPT = LC < kEPT ? LC : (LC / kNT > kEPT ? LC / kNT : kEPT);
+  static constexpr int EPT = LC == 1024 ? JF_EPT1024
+                                        : (LC < kEPT ? LC : (LC / kNT > kEPT ? LC / kNT : kEPT));
   static constexpr int GMAX = ilog2(EPT);
   static constexpr int TPC = LC / EPT;  // threads per column (divides 64 when <= 64)
   static constexpr int T = kNT / TPC;   // columns per workgroup

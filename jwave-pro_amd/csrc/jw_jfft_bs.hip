@@ -148,6 +148,62 @@ struct BMid {  // a[i].mul(b[i]) (:300-302)
   __device__ cplx operator()(int, long, long i, cplx x) const { return jmul(x, B[i]); }
 };
 
+// A three-pass transform's output (pass 3) times B: a[i].mul(b[i]) (:300-302)
+struct OutMulB {
+  cplx* p;
+  long st;
+  const cplx* B;
+  __device__ void operator()(long it, long i, cplx v) const { p[it * st + i] = jmul(v, B[i]); }
+};
+
+// The convolution of fftBluestein with three-pass m-point transforms (m >= three_pass_min(),
+// up to 2^28): FFT_m(a) = passes 1..3 (the last one multiplying by B), IFFT_m of the product =
+// passes 1..3 into Post.  Same operations in the same order as the two-pass chain below.
+int bs_conv3(long m, long items, const Pre& pre, const Post& post, const cplx* B,
+             StreamAllocs& mem, hipStream_t s) {
+  Tw3 twf, twi;
+  int st = twiddles3(m, false, &twf, mem, s);
+  if (st == JW_OK) st = twiddles3(m, true, &twi, mem, s);
+  if (st != JW_OK) return st;
+  const int abits = ilog2(twf.A), cbits = ilog2(twf.C);
+  const long ab = (long)twf.A * twf.B;
+  const long chunk = std::max(1L, std::min<long>(items, (2L << 30) / (2 * m * (long)sizeof(cplx))));
+  cplx *Z = nullptr, *Zi = nullptr;
+  JW_HIP_TRY(mem.alloc(&Z, (size_t)chunk * m * sizeof(cplx)));
+  JW_HIP_TRY(mem.alloc(&Zi, (size_t)chunk * m * sizeof(cplx)));
+  auto three = [&](auto in, auto out, const Tw3& tw, cplx* work, long ni) -> int {
+    int r = with_big_lc(tw.A, [&](auto LCc) -> int {
+      constexpr int LC = decltype(LCc)::value;
+      return launch_grid<LC>(kp1<LC, decltype(in), OutC>, (m / tw.A / Geo<LC>::T) * ni, s, in,
+                             OutC{work, m}, ilog2(m / tw.A), ni, tw.p1);
+    });
+    if (r == JW_OK)
+      r = with_big_lc(tw.B, [&](auto LCc) -> int {
+        constexpr int LC = decltype(LCc)::value;
+        const Plane pl{work, m, ab, cbits};
+        return launch_grid<LC>(kp2s<LC, Plane, Plane>, (tw.A / Geo<LC>::T) * ni * tw.C, s, pl, pl,
+                               abits, ni * tw.C, tw.pm);
+      });
+    if (r == JW_OK)
+      r = with_big_lc(tw.C, [&](auto LCc) -> int {
+        constexpr int LC = decltype(LCc)::value;
+        return launch_grid<LC>(kp2s<LC, RowsC, decltype(out)>, (ab / Geo<LC>::T) * ni, s,
+                               RowsC{work, m}, out, ilog2(ab), ni, tw.p3);
+      });
+    return r;
+  };
+  for (long i0 = 0; i0 < items && st == JW_OK; i0 += chunk) {
+    const long ni = std::min(chunk, items - i0);
+    Pre pc = pre;
+    pc.it0 += i0;
+    Post qc = post;
+    qc.it0 += i0;
+    st = three(pc, OutMulB{Zi, m, B}, twf, Z, ni);            // FFT_m(a), times B (:293-302)
+    if (st == JW_OK) st = three(RowsC{Zi, m}, qc, twi, Z, ni);  // IFFT_m, post (:303-321)
+  }
+  return st;
+}
+
 // `items` Bluestein transforms of length n: pre supplies x (before the chirp), post receives
 // the results (both get the tables filled in here).  Workspaces are this call's own
 // (stream-ordered: released after the kernels queued here have used them).
@@ -163,6 +219,7 @@ int bs_rows(long n, bool inverse, long items, Pre pre, Post post, StreamAllocs& 
   post.inv_m = 1.0 / (double)m;
   post.inv_n = 1.0 / (double)n;
   post.inverse = inverse ? 1 : 0;
+  if (m > kLineMax && m >= three_pass_min()) return bs_conv3(m, items, pre, post, T.B, mem, s);
   const int lc1 = split_lc1(m);
   Tw twf, twi;
   if ((st = twiddles(m, false, lc1, &twf, mem, s)) != JW_OK) return st;

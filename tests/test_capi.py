@@ -356,14 +356,15 @@ def test_fft_levels_past_2_23_are_unsupported_not_direct():
     # JWave runs these levels through its FFT convolution (MODWTTransform.java:640-664,
     # FastFourierTransform.java:112-164); the engine's FFT paths stop at 2^23, so the call must
     # fail with the limit named instead of returning DIRECT values (~1e-10 away).
+    # STRICT (JWave's FFT): powers of two to 2^28, Bluestein to 2^27; FMA's pyramid: 2^23
     lib = _native.lib()
-    n, J = (1 << 23) + 2, 2
-    x = np.zeros(n)
-    c = np.empty((J + 1) * n)
+    J = 2
     vp = ctypes.c_void_p
-    for arith, method in ((_native.JW_ARITH_STRICT, _native.JW_CONV_AUTO),
-                          (_native.JW_ARITH_STRICT, _native.JW_CONV_FFT),
-                          (_native.JW_ARITH_FMA, _native.JW_CONV_FFT)):
+    for arith, method, n, lim in ((_native.JW_ARITH_STRICT, _native.JW_CONV_AUTO, (1 << 27) + 2, "2^27"),
+                                  (_native.JW_ARITH_STRICT, _native.JW_CONV_FFT, (1 << 27) + 2, "2^27"),
+                                  (_native.JW_ARITH_FMA, _native.JW_CONV_FFT, (1 << 23) + 2, "2^23")):
+        x = np.zeros(n)  # calloc / untouched pages: nothing is read before the check
+        c = np.zeros((J + 1) * n)
         wv = W.Daubechies4()
         sd, wd = np.asarray(wv.getScalingDeComposition()), np.asarray(wv.getWaveletDeComposition())
         plan = vp()
@@ -373,22 +374,24 @@ def test_fft_levels_past_2_23_are_unsupported_not_direct():
             st = fn(plan, vp(a.ctypes.data), vp(b.ctypes.data), n, J, 1, method, _native.JW_HOST, None)
             assert st == _native.JW_ERR_UNSUPPORTED, (arith, method, st)
             msg = _native.last_error()
-            assert "2^23" in msg and str(n) in msg and "level 1" in msg, msg
+            assert lim in msg and str(n) in msg and "level 1" in msg, msg
         lib.jw_modwt_plan_destroy(plan)
+        del x, c
     # the Python mirror raises it (NotImplementedError), never a DIRECT result
-    m = MODWTTransform(W.Daubechies4())
+    m = MODWTTransform(W.Daubechies4(), arith="fma")
+    m.setConvolutionMethod(MODWTTransform.ConvolutionMethod.FFT)
     with pytest.raises(NotImplementedError, match="2\\^23"):
-        m.forwardMODWT(x, J)
+        m.forwardMODWT(np.zeros((1 << 23) + 2), J)
 
 
 def test_strict_fft_past_its_range_is_unsupported():
     # STRICT runs the reference's FFT for powers of two up to 2^28 (three column passes past
-    # 2^24) and Bluestein up to 2^23; past those, an error naming the limits
+    # 2^24) and Bluestein up to 2^27 (m <= 2^28); past those, an error naming the limits
     lib = _native.lib()
     vp = ctypes.c_void_p
-    for n in ((1 << 23) + 2, 1 << 29):
+    for n in ((1 << 27) + 2, 1 << 29):
         z = np.zeros(2 * n)  # calloc: pages untouched
         st = lib.jw_fft_forward_ex(vp(z.ctypes.data), vp(z.ctypes.data), n, 1,
                                    _native.JW_ARITH_STRICT, _native.JW_HOST, None)
         msg = _native.last_error()
-        assert st == _native.JW_ERR_UNSUPPORTED and "2^28" in msg and "2^23" in msg, msg
+        assert st == _native.JW_ERR_UNSUPPORTED and "2^28" in msg and "2^27" in msg, msg

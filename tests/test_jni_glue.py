@@ -167,9 +167,11 @@ def test_engine_entries_without_a_device(jni):
 def test_unsupported_maps_to_unsupported_operation(jni):
     # JW_ERR_UNSUPPORTED (an FFT level past the engine's FFT range) ->
     # java.lang.UnsupportedOperationException carrying the limit
-    p = _modwt_plan(jni)
+    wv = W.Daubechies4()
+    p = jni.call("HipMODWTTransform_nPlanCreate", jni.darray(wv.getScalingDeComposition()),
+                 jni.darray(wv.getWaveletDeComposition()), 4096, 1)  # ARITH_FMA
     n = (1 << 23) + 2
-    with pytest.raises(JavaException) as e:
-        jni.call("HipMODWTTransform_nForward", p, jni.darray(np.zeros(n)), 2, 0)
+    with pytest.raises(JavaException) as e:  # ConvolutionMethod.FFT past the pyramid's 2^23
+        jni.call("HipMODWTTransform_nForward", p, jni.darray(np.zeros(n)), 2, 2)
     assert e.value.cls == "java/lang/UnsupportedOperationException" and "2^23" in e.value.msg
     jni.call("HipMODWTTransform_nPlanDestroy", p)

@@ -261,3 +261,29 @@ def test_fft_strict_2_25():
     z = rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n)
     X = FastFourierTransform().forwardComplex(z)
     assert bits_equal(X.view(np.float64), orc.fft(z).view(np.float64))
+
+
+@pytest.mark.parametrize("n", [70001, 200001])
+def test_bluestein_three_pass_bit_exact(n, monkeypatch):
+    # Bluestein's m-point convolution on three-pass transforms (jw_jfft_bs.hip bs_conv3): the
+    # path of non-power-of-two lengths past 2^23 (m > 2^24), at lengths the oracle runs quickly
+    monkeypatch.setenv("JW_JFFT_3PASS_MIN", str(1 << 18))
+    rng = np.random.default_rng(n)
+    z = rng.uniform(-1, 1, (2, n)) + 1j * rng.uniform(-1, 1, (2, n))
+    f = FastFourierTransform()
+    X = f.forwardComplex(z)
+    for b in range(2):
+        assert bits_equal(X[b].view(np.float64), orc.fft(z[b]).view(np.float64)), b
+    zr = f.reverseComplex(X)
+    for b in range(2):
+        assert bits_equal(zr[b].view(np.float64), orc.fft(X[b], inverse=True).view(np.float64)), b
+    wv = W.Daubechies4()
+    g, h = ofilters(wv)
+    xs = np.stack([orc.fill_uniform(n, 9 + b) for b in range(2)])
+    m = MODWTTransform(wv)  # AUTO
+    c = m.forwardMODWT(xs, 3)
+    xr = m.inverseMODWT(c)
+    for b in range(2):
+        ref = orc.modwt_forward(xs[b], 3, g, h, "auto")
+        assert bits_equal(c[b], ref), b
+        assert bits_equal(xr[b], orc.modwt_inverse(ref, g, h, "auto")), b
