@@ -394,6 +394,11 @@ constexpr int kRowMaxM = 20;  // longer filters keep the runtime-level kernels (
 #ifndef JW_REV_PAIRS2
 #define JW_REV_PAIRS2 1
 #endif
+#ifndef JW_REV_SMALL_WAVE
+#define JW_REV_SMALL_WAVE 1
+#endif
+// row reverse: levels 2 .. 128 on one wave with wave-level syncs (A/B builds: 0)
+constexpr bool kRevSmallWave = JW_REV_SMALL_WAVE;
 constexpr bool kRevPairs2 = JW_REV_PAIRS2;  // row kernels: two outputs per lane (A/B builds: 0)
 
 template <bool FMA, int M, int H>
@@ -544,9 +549,21 @@ __device__ __forceinline__ void rev_two_pairs(const double* buf, int half, int u
   o1 = d2{b0, b1};
 }
 
-template <bool FMA, int M, int KIND, int H>
+// Within one wavefront the DS instructions execute in issue order: a wave-scope fence pair
+// around a wave barrier keeps the compiler from moving LDS accesses across it.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One reverse level of a 4096-sample row.  WAVE: a level with half <= 64 output pairs run by
+// wave 0 alone with wave-level syncs (the caller issues one workgroup barrier after the last
+// such level), instead of two workgroup barriers per level.
+template <bool FMA, int M, int KIND, int H, bool WAVE = false>
 __device__ __forceinline__ void row_rev_level(double* buf, double* xs, int tid, const Filters& f,
                                               const d2* tp) {
+  static_assert(!WAVE || H <= 128, "wave-level reverse levels: half <= 64");
   constexpr int half = H / 2, P = half >= kNT2 ? half / kNT2 : 1;
   d2 o[P];
   if constexpr (FMA && H >= M && P >= 2 && kRevPairs2) {
@@ -637,13 +654,31 @@ __device__ __forceinline__ void row_rev_level(double* buf, double* xs, int tid, 
     for (int r = 0; r < P; ++r) *(d2*)&xs[2 * (tid + r * kNT2)] = o[r];
     return;
   }
-  __syncthreads();
+  if constexpr (WAVE) {
+    wave_sync();
+  } else {
+    __syncthreads();
+  }
 #pragma unroll
   for (int r = 0; r < P; ++r) {
     const int u = tid + r * kNT2;
     if (half >= kNT2 || u < half) *(d2*)&buf[2 * u] = o[r];
   }
-  __syncthreads();
+  if constexpr (WAVE) {
+    wave_sync();
+  } else {
+    __syncthreads();
+  }
+}
+
+// Levels H, 2H, .., 128 from h0 on, wave 0 only (WAVE levels)
+template <bool FMA, int M, int KIND, int H>
+__device__ __forceinline__ void row_rev_small(double* buf, int tid, int h0, const Filters& f,
+                                              const d2* tp) {
+  if constexpr (H <= 128) {
+    if (H >= h0) row_rev_level<FMA, M, KIND, H, true>(buf, nullptr, tid, f, tp);
+    row_rev_small<FMA, M, KIND, 2 * H>(buf, tid, h0, f, tp);
+  }
 }
 
 // Levels H, 2H, ..., kRowN from h0 on (h0 a power of two); true when the last one stored to xs.
@@ -685,8 +720,19 @@ __global__ __launch_bounds__(kNT2) void fwt_rev_row(const double* y, double* x, 
   }
   __syncthreads();
   // cascade_rev's loop: h = h0, 2 h0, ... while h <= n, h >= tw, h >= 2 (h0 >= tw here)
-  const bool stored = h0 >= tw && h0 >= 2 && h0 <= kRowN &&
-                      row_rev_from<FMA, M, KIND, 2>(buf, xs, tid, h0, f, tp);
+  const bool run = h0 >= tw && h0 >= 2 && h0 <= kRowN;
+  bool stored = false;
+  if (run) {
+    if (kRevSmallWave) {  // levels 2 .. 128 by wave 0, then one workgroup barrier
+      if (h0 <= 128) {
+        if (tid < 64) row_rev_small<FMA, M, KIND, 2>(buf, tid, h0, f, tp);
+        __syncthreads();
+      }
+      stored = row_rev_from<FMA, M, KIND, 256>(buf, xs, tid, h0, f, tp);
+    } else {
+      stored = row_rev_from<FMA, M, KIND, 2>(buf, xs, tid, h0, f, tp);
+    }
+  }
   if (!stored)
     for (int i = 2 * tid; i < kRowN; i += 2 * kNT2) *(d2*)&xs[i] = *(const d2*)&buf[i];
 }
