@@ -168,6 +168,51 @@ int filter_spectra(const ModwtPlan& p, long N, int J, const cplx** F, StreamAllo
 const cplx* spec_h(const cplx* F, long N, int j) { return F + (long)(2 * (j - 1)) * N; }
 const cplx* spec_g(const cplx* F, long N, int j) { return F + (long)(2 * (j - 1) + 1) * N; }
 
+// The spectra again, each row stored per column of the two-pass kp2p view: FT[q][l C + h] =
+// F[q][h R + l] (R columns of C points), so that a column's products read consecutive entries.
+// Cached beside F per (device, N, J, taps, R).  env JW_AUTO_SPECT=0: natural order (A/B runs).
+using SpecTKey = std::tuple<int, long, int, long, std::vector<double>>;
+DevCache<SpecTKey> g_spect(kCacheBytes);
+
+__global__ __launch_bounds__(256) void kspec_t(const cplx* __restrict__ F, cplx* __restrict__ FT,
+                                               long N, int rbits, long C) {
+  __shared__ cplx t[32][33];
+  const long R = 1L << rbits;
+  const long q = blockIdx.z;
+  const long h0 = (long)blockIdx.y * 32, l0 = (long)blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int k = ty; k < 32; k += 8) t[k][tx] = F[q * N + (h0 + k) * R + l0 + tx];
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) FT[q * N + (l0 + k) * C + h0 + tx] = t[tx][k];
+}
+
+bool spect_enabled() {
+  const char* e = std::getenv("JW_AUTO_SPECT");
+  return !(e && e[0] == '0');
+}
+
+int spectra_t(const ModwtPlan& p, long N, int J, const cplx* F, long R, const cplx** FT,
+              StreamAllocs& mem, hipStream_t s) {
+  int dev = 0;
+  JW_HIP_TRY(hipGetDevice(&dev));
+  std::vector<double> taps(p.g, p.g + p.L);
+  taps.insert(taps.end(), p.h, p.h + p.L);
+  const long C = N / R;
+  const void* out = nullptr;
+  const int st = cached_table(g_spect, SpecTKey(dev, N, J, R, taps),
+                              (size_t)2 * J * N * sizeof(cplx), mem, s, &out, [&](void* d) -> int {
+                                if (R < 32 || C < 32)
+                                  return fail(JW_ERR_UNSUPPORTED, "spectra_t: %ld x %ld", R, C);
+                                hipLaunchKernelGGL(kspec_t, dim3((unsigned)(R / 32), (unsigned)(C / 32),
+                                                                 (unsigned)(2 * J)),
+                                                   dim3(256), 0, s, F, (cplx*)d, N, ilog2(R), C);
+                                JW_HIP_TRY(hipGetLastError());
+                                return JW_OK;
+                              });
+  *FT = (const cplx*)out;
+  return st;
+}
+
 // ---------------------------------------------------------------------------------------
 // MODWT, one level per step as MODWTTransform.forwardMODWT / inverseMODWT run it (:290-304,
 // :355-372): FFT levels here, DIRECT levels through the direct per-level kernels (jw_modwt.hip).
@@ -251,9 +296,9 @@ bool kp2p_both_filters() {
 // Z (nb x [C][R], forward pass-1 rows of V_{j-1}) -> Zi_h, Zi_g (inverse pass-1 rows) -> W_j,
 // and V_j either stored (last level, or a DIRECT level next) or run straight into the next
 // level's pass 1 (Z).
-int forward_cols(const ModwtPlan& p, const bool* fft, const cplx* F, const Tw& twf,
-                 const Tw& twi, const ColGeo& g, const double* x, double* coeffs, const Chunk& c,
-                 cplx* Z, cplx* Zi, hipStream_t s) {
+int forward_cols(const ModwtPlan& p, const bool* fft, const cplx* F, const cplx* FT,
+                 const Tw& twf, const Tw& twi, const ColGeo& g, const double* x, double* coeffs,
+                 const Chunk& c, cplx* Z, cplx* Zi, hipStream_t s) {
   const long N = c.N, nb = c.nb, rs = (long)(c.J + 1) * N;
   const double* vin = x;
   long vs = N;
@@ -287,6 +332,11 @@ int forward_cols(const ModwtPlan& p, const bool* fft, const cplx* F, const Tw& t
         return launch_grid<LC>(kp2p<LC, 2, RowsC, FwdMid2, OutF>, (g.R / Geo<LC>::T) * nb, s,
                                RowsC{Z, N}, FwdMid2{spec_h(F, N, j), spec_g(F, N, j)},
                                OutF{Zi, N, nb * N}, g.rbits, nb, twf.p2, twi.p1);
+      if (FT)
+        return launch_grid<LC>(kp2p<LC, 1, ZPair, FwdMidT, OutPair>, (g.R / Geo<LC>::T) * 2 * nb,
+                               s, ZPair{Z, N},
+                               FwdMidT{spec_h(FT, N, j), spec_g(FT, N, j), g.rbits, g.C},
+                               OutPair{Zi, N, nb * N}, g.rbits, 2 * nb, twf.p2, twi.p1);
       return launch_grid<LC>(kp2p<LC, 1, ZPair, FwdMid, OutPair>, (g.R / Geo<LC>::T) * 2 * nb, s,
                              ZPair{Z, N}, FwdMid{spec_h(F, N, j), spec_g(F, N, j)},
                              OutPair{Zi, N, nb * N}, g.rbits, 2 * nb, twf.p2, twi.p1);
@@ -315,9 +365,9 @@ int forward_cols(const ModwtPlan& p, const bool* fft, const cplx* F, const Tw& t
 }
 
 // Zs = [Z_V | Z_W] (forward pass-1 rows of V_j and W_j), Zi = [Zi_A | Zi_D]
-int inverse_cols(const ModwtPlan& p, const bool* fft, const cplx* F, const Tw& twf,
-                 const Tw& twi, const ColGeo& g, const double* coeffs, double* x, const Chunk& c,
-                 cplx* Zs, cplx* Zi, hipStream_t s) {
+int inverse_cols(const ModwtPlan& p, const bool* fft, const cplx* F, const cplx* FT,
+                 const Tw& twf, const Tw& twi, const ColGeo& g, const double* coeffs, double* x,
+                 const Chunk& c, cplx* Zs, cplx* Zi, hipStream_t s) {
   const long N = c.N, nb = c.nb, rs = (long)(c.J + 1) * N;
   const double* vin = coeffs + (long)c.J * N;
   long vs = rs;
@@ -347,6 +397,11 @@ int inverse_cols(const ModwtPlan& p, const bool* fft, const cplx* F, const Tw& t
     if (st != JW_OK) break;
     st = with_big_lc(g.C, [&](auto LCc) -> int {
       constexpr int LC = decltype(LCc)::value;
+      if (FT)
+        return launch_grid<LC>(kp2p<LC, 1, RowsC, AdjMidT, OutF>, (g.R / Geo<LC>::T) * 2 * nb, s,
+                               RowsC{Zs, N},
+                               AdjMidT{spec_g(FT, N, j), spec_h(FT, N, j), nb, g.rbits, g.C},
+                               OutF{Zi, N, 0}, g.rbits, 2 * nb, twf.p2, twi.p1);
       return launch_grid<LC>(kp2p<LC, 1, RowsC, AdjMid, OutF>, (g.R / Geo<LC>::T) * 2 * nb, s,
                              RowsC{Zs, N}, AdjMid{spec_g(F, N, j), spec_h(F, N, j), nb},
                              OutF{Zi, N, 0}, g.rbits, 2 * nb, twf.p2, twi.p1);
@@ -485,6 +540,8 @@ int modwt_strict(bool inverse, const ModwtPlan& p, const double* in, double* out
   Tw twf, twi;  // forward FFTs split R x C, inverse FFTs C x R
   if ((st = twiddles(N, false, (int)g.R, &twf, mem, s)) != JW_OK) return st;
   if ((st = twiddles(N, true, (int)g.C, &twi, mem, s)) != JW_OK) return st;
+  const cplx* FT = nullptr;  // the spectra per kp2p column (kp2p's view is [C][R])
+  if (spect_enabled() && (st = spectra_t(p, N, J, F, g.R, &FT, mem, s)) != JW_OK) return st;
   // per signal: 4 complex rows of workspace (forward uses 3) + 2 real scratch rows
   const long per_sig = 4 * N * (long)sizeof(cplx) + 2 * N * (long)sizeof(double);
   const long chunk = std::max(1L, std::min<long>(batch, (4L << 30) / per_sig));
@@ -495,9 +552,9 @@ int modwt_strict(bool inverse, const ModwtPlan& p, const double* in, double* out
   for (long b0 = 0; b0 < batch && st == JW_OK; b0 += chunk) {
     const long nb = std::min(chunk, batch - b0);
     const Chunk c{nb, N, J, {tmp, tmp + chunk * N}};
-    st = inverse ? inverse_cols(p, fft, F, twf, twi, g, in + b0 * rs, out + b0 * N, c, W,
+    st = inverse ? inverse_cols(p, fft, F, FT, twf, twi, g, in + b0 * rs, out + b0 * N, c, W,
                                 W + 2 * nb * N, s)
-                 : forward_cols(p, fft, F, twf, twi, g, in + b0 * N, out + b0 * rs, c, W,
+                 : forward_cols(p, fft, F, FT, twf, twi, g, in + b0 * N, out + b0 * rs, c, W,
                                 W + nb * N, s);
   }
   return st;

@@ -186,6 +186,31 @@ struct FwdMid {
     return jmul(x, ((it & 1) ? fg : fh)[i]);
   }
 };
+// The same products with the filter spectra stored per column of the kp2p view (FT[l C + h] =
+// F[h R + l], l < R columns, h < C points; jw_jfft.hip spectra_t): the lanes of a column read
+// consecutive entries instead of one 16-byte value per 16 KB row (natural order).
+struct FwdMidT {
+  const cplx* fh;
+  const cplx* fg;
+  int rbits;
+  long C;
+  __device__ cplx operator()(int, long it, long i, cplx x) const {
+    const long t = (i & ((1L << rbits) - 1)) * C + (i >> rbits);
+    return jmul(x, ((it & 1) ? fg : fh)[t]);
+  }
+};
+struct AdjMidT {
+  const cplx* fg;
+  const cplx* fh;
+  long nb;
+  int rbits;
+  long C;
+  __device__ cplx operator()(int, long it, long i, cplx x) const {
+    const long t = (i & ((1L << rbits) - 1)) * C + (i >> rbits);
+    const cplx f = (it < nb ? fg : fh)[t];
+    return jmul(x, make_double2(f.x, -f.y));
+  }
+};
 // forward level, both filters per item (kp2p NF = 2): f = 0 -> h_j (W_j), 1 -> g_j (V_j)
 struct FwdMid2 {
   const cplx* fh;
