@@ -521,13 +521,19 @@ struct SideStream {
   int dev = -1;
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
+  // A/B runs (JW_CWT_PRIO=1): the two-pass chain on a high-priority stream beside the band
+  // kernel, so its 270 short dependent launches are dispatched ahead of the band's workgroups
+  hipStream_t hi = nullptr;
+  hipEvent_t hi_join = nullptr;
   ~SideStream() {
     if (dev < 0) return;
     (void)hipSetDevice(dev);
-    if (s) (void)hipStreamSynchronize(s);
-    if (fork) (void)hipEventDestroy(fork);
-    if (join) (void)hipEventDestroy(join);
-    if (s) (void)hipStreamDestroy(s);
+    for (hipStream_t t : {s, hi})
+      if (t) (void)hipStreamSynchronize(t);
+    for (hipEvent_t e : {fork, join, hi_join})
+      if (e) (void)hipEventDestroy(e);
+    for (hipStream_t t : {s, hi})
+      if (t) (void)hipStreamDestroy(t);
   }
 };
 static int side_stream(SideStream** out) {
@@ -541,6 +547,10 @@ static int side_stream(SideStream** out) {
     JW_HIP_TRY(hipStreamCreateWithFlags(&ss->s, hipStreamNonBlocking));
     JW_HIP_TRY(hipEventCreateWithFlags(&ss->fork, hipEventDisableTiming));
     JW_HIP_TRY(hipEventCreateWithFlags(&ss->join, hipEventDisableTiming));
+    int least = 0, greatest = 0;
+    JW_HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    JW_HIP_TRY(hipStreamCreateWithPriority(&ss->hi, hipStreamNonBlocking, greatest));
+    JW_HIP_TRY(hipEventCreateWithFlags(&ss->hi_join, hipEventDisableTiming));
     sides[dev] = std::move(ss);
   }
   *out = sides[dev].get();
@@ -551,8 +561,10 @@ static int side_stream(SideStream** out) {
 struct JoinGuard {
   hipStream_t s = nullptr;
   SideStream* side = nullptr;
+  bool hi = false;  // the two-pass chain ran on side->hi
   ~JoinGuard() {
     if (side) (void)hipStreamWaitEvent(s, side->join, 0);
+    if (side && hi) (void)hipStreamWaitEvent(s, side->hi_join, 0);
   }
 };
 
@@ -782,6 +794,16 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     JW_HIP_TRY(hipGetLastError());
     if (join.side) JW_HIP_TRY(hipEventRecord(join.side->join, bs));
   }
+  // A/B runs: the two-pass chain on the side's high-priority stream (forked after the spectra)
+  hipStream_t ps = s;
+  {
+    const char* gpr = std::getenv("JW_CWT_PRIO");
+    if (join.side && pairs > 0 && gpr && gpr[0] == '1') {
+      JW_HIP_TRY(hipStreamWaitEvent(join.side->hi, join.side->fork, 0));
+      ps = join.side->hi;
+      join.hi = true;
+    }
+  }
   // the other (signal, scale) pairs: IFFT(X * psi_hat) -> coefficients in two passes
   if (pipe && st == JW_OK) {
     auto go = [&](auto kind) {
@@ -792,7 +814,7 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
       auto mk_out = [&](long p0) {
         return CoefOut{out, n, N1, p0, 1.0 / (double)N, (ntm & 2) != 0, pmf};
       };
-      return fft::run_fft512_pipelined<1>(N, pairs, gpair, mk_in, mk_out, A, A + gpair * N, s, T,
+      return fft::run_fft512_pipelined<1>(N, pairs, gpair, mk_in, mk_out, A, A + gpair * N, ps, T,
                                           (ntm & 1) != 0);
     };
     switch (wavelet) {
@@ -803,6 +825,7 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
       default: st = go(std::integral_constant<int, JW_CWT_MEYER>{}); break;
     }
   }
+  if (join.hi) JW_HIP_TRY(hipEventRecord(join.side->hi_join, ps));
   for (long p0 = 0; p0 < pairs && st == JW_OK && !pipe; p0 += gpair) {
     const long np_ = std::min<long>(gpair, pairs - p0);
     CoefOut o{out, n, N <= 4096 ? 1 : N1, p0, 1.0 / (double)N, (ntm & 2) != 0, pmf};
