@@ -259,11 +259,19 @@ __global__ __launch_bounds__(kNT) void kp2s(In in, Out out, int wbits, long nite
   store_cols<LC>(lds, out, item, c0, wbits);
 }
 
+#ifndef JF_KP2R_SCHED
+#define JF_KP2R_SCHED 0
+#endif
+#ifndef JF_KP2R_WPE
+#define JF_KP2R_WPE 4
+#endif
 // pass 2, then NF pointwise products (Mid: cplx operator()(int f, long item, long i, cplx X),
 // i = the natural index h W + l), each run through pass 1 of the next transform (table tw1)
 // and stored as rows (Out: operator()(int f, long item, long j, cplx v), j = row LC + pos).
 template <int LC, int NF, class In, class Mid, class Out>
-__global__ __launch_bounds__(kNT) void kp2p(In in, Mid mid, Out out, int wbits, long nitems,
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(NF == 1 ? JF_KP2R_WPE
+                                                                             : 1))) void kp2p(
+    In in, Mid mid, Out out, int wbits, long nitems,
                                             const cplx* __restrict__ tw2,
                                             const cplx* __restrict__ tw1) {
   using G = Geo<LC>;
@@ -295,7 +303,11 @@ __global__ __launch_bounds__(kNT) void kp2p(In in, Mid mid, Out out, int wbits, 
       col[pidx(brev(h, G::LOG))] = mid(f, item, ((long)h << wbits) + l, X[k]);
     }
     col_sync<LC>();
-    run_stages<LC>(col, tl, tw1);
+    // every product runs the same pass-1 twiddles: opaque per product, or the compiler holds
+    // the first product's twiddle values for the next (NF = 2: 208 VGPRs)
+    const cplx* tw1f = tw1;
+    if (NF > 1) asm volatile("" : "+v"(tw1f));
+    run_stages<LC>(col, tl, tw1f);
     __syncthreads();
     store_rows<LC>(lds, [&](long it, long j, cplx v) { out(f, it, j, v); }, item, c0, wbits);
   }
@@ -308,8 +320,12 @@ __global__ __launch_bounds__(kNT) void kp2p(In in, Mid mid, Out out, int wbits, 
 // (as Complex(v, 0)) runs through pass 1 of the next forward transform (table tw1f) and is
 // stored as rows (Out: operator()(long item, long j, cplx v)); otherwise Out
 // (operator()(long item, long i, double v)) stores it at natural index i.
+// waves_per_eu(4): the LDS allows four waves per SIMD; the fused two-input form fits 128 VGPRs
+// with no spill (the unfused one spilled 20, so it keeps its own allocation)
 template <int LC, int NIN, bool FUSE, class In, class Post, class Out>
-__global__ __launch_bounds__(kNT) void kp2r(In in, Post post, Out out, int wbits, long nitems,
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(
+    NIN == 1 || FUSE ? JF_KP2R_WPE : 1))) void kp2r(
+    In in, Post post, Out out, int wbits, long nitems,
                                             const cplx* __restrict__ tw2,
                                             const cplx* __restrict__ tw1f) {
   using G = Geo<LC>;
@@ -327,7 +343,12 @@ __global__ __launch_bounds__(kNT) void kp2r(In in, Post post, Out out, int wbits
     if (s > 0) __syncthreads();
     load_cols<LC, false>(lds, [&](long it, long i) { return in(s, it, i); }, item, c0, wbits);
     __syncthreads();
-    run_stages<LC>(col, tl, tw2 + l * LC);
+    // both inputs use the same twiddles: an opaque pointer per input keeps the compiler from
+    // holding the first input's twiddle values for the second (NIN = 2 took 210 VGPRs, two
+    // waves per SIMD, instead of ~120)
+    const cplx* tws = tw2 + l * LC;
+    if (NIN > 1) asm volatile("" : "+v"(tws));
+    run_stages<LC>(col, tl, tws);
     col_sync<LC>();
 #pragma unroll
     for (int k = 0; k < G::EPT; ++k) {
@@ -335,6 +356,8 @@ __global__ __launch_bounds__(kNT) void kp2r(In in, Post post, Out out, int wbits
       const double v = post(s, item, ((long)h << wbits) + l, col[pidx(h)]);
       acc[k] = s == 0 ? v : acc[k] + v;
     }
+    // keep the next input's loads behind this one's stages (register pressure, A/B builds)
+    if (JF_KP2R_SCHED) __builtin_amdgcn_sched_barrier(0);
   }
   col_sync<LC>();
   if constexpr (FUSE) {
