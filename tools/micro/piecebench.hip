@@ -75,6 +75,8 @@ int main() {
   CK(hipMalloc(&b, (size_t)pairs * 262144 * 16));
   CK(hipMemset(a, 0, (size_t)pairs * 262144 * 16));
   CK(hipMemset(b, 0x3c, (size_t)pairs * 262144 * 16));
+  run<2>(a, b, pairs);
+  run<4>(a, b, pairs);
   run<8>(a, b, pairs);
   run<16>(a, b, pairs);
   run<32>(a, b, pairs);
