@@ -131,6 +131,18 @@ class Harness:
             return cls.value.decode(), msg.value.decode()
         return None
 
+    def new_env(self):
+        """A separate JNIEnv (a JVM gives every thread its own)."""
+        return vp(self.L.mock_env_new())
+
+    def call_env(self, env, name, *args):
+        """call() on a given environment (per-thread use); returns (result, exception or None)."""
+        r = self.fns[name](env, None, *args)
+        cls, msg = ctypes.create_string_buffer(128), ctypes.create_string_buffer(512)
+        if self.L.mock_exception(env, cls, 128, msg, 512):
+            return r, (cls.value.decode(), msg.value.decode())
+        return r, None
+
     def call(self, name, *args):
         """Calls Java_jwave_hip_<name>(env, class, *args); raises JavaException when the glue
         left one pending (and asserts it returned nothing then)."""

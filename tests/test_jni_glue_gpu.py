@@ -152,3 +152,47 @@ def test_engine_device_entries(jni):
         jni.call("HipEngine_nSetDevice", 4096)
     assert e.value.cls == "java/lang/IllegalArgumentException" and "out of range" in e.value.msg
     assert jni.call("HipEngine_nReleaseCaches") >= 0
+
+
+def test_glue_from_threads_on_one_plan(jni):
+    # MODWTThreadSafetyTest.java:23-104 through the glue: one shared plan, four threads, each with
+    # its own JNIEnv (as a JVM gives them), forward + inverse of its own signals, every result
+    # bit-exact against the oracle
+    import threading
+    wv = W.Daubechies4()
+    g, h = orc.modwt_filters(wv.getScalingDeComposition(), wv.getWaveletDeComposition())
+    p = _modwt_plan(jni, wv)
+    errors = []
+    inputs = {t: orc.fill_uniform(8192 + 512 * t, 100 + t) for t in range(4)}
+    refs = {t: orc.modwt_forward(inputs[t], 6, g, h, "direct_nz") for t in range(4)}
+
+    def worker(t):
+        env = jni.new_env()
+        try:
+            for it in range(3):
+                method = 0 if it == 2 else 1  # AUTO on the last pass (JWave's FFT path)
+                c, exc = jni.call_env(env, "HipMODWTTransform_nForward", p, jni.darray(inputs[t]), 6,
+                                      method)
+                if exc:
+                    errors.append((t, exc))
+                    return
+                got = jni.read(c)
+                ref = refs[t] if method == 1 else orc.modwt_forward(inputs[t], 6, g, h, "auto")
+                if not bits_equal(got, ref):
+                    errors.append((t, it, "forward differs"))
+                xr, exc = jni.call_env(env, "HipMODWTTransform_nInverse", p, jni.matrix(got), method)
+                if exc or not bits_equal(jni.read(xr),
+                                         orc.modwt_inverse(ref, g, h, "direct_nz" if method == 1
+                                                           else "auto")):
+                    errors.append((t, it, "inverse differs", exc))
+        finally:
+            jni.L.mock_env_free(env)
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=100)
+    assert not any(th.is_alive() for th in ths)
+    assert not errors, errors
+    jni.call("HipMODWTTransform_nPlanDestroy", p)
