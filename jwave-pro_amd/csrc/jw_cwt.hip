@@ -525,15 +525,35 @@ struct SideStream {
   // kernel, so its 270 short dependent launches are dispatched ahead of the band's workgroups
   hipStream_t hi = nullptr;
   hipEvent_t hi_join = nullptr;
+  // A/B runs (JW_CWT_CUS=k, 1..7): the band kernel on a stream limited to k of every 8 CUs and
+  // the two-pass chain on one limited to the other 8 - k (hipExtStreamCreateWithCUMask)
+  int cus = 0;
+  hipStream_t mband = nullptr, mtwo = nullptr;
   ~SideStream() {
     if (dev < 0) return;
     (void)hipSetDevice(dev);
-    for (hipStream_t t : {s, hi})
+    for (hipStream_t t : {s, hi, mband, mtwo})
       if (t) (void)hipStreamSynchronize(t);
     for (hipEvent_t e : {fork, join, hi_join})
       if (e) (void)hipEventDestroy(e);
-    for (hipStream_t t : {s, hi})
+    for (hipStream_t t : {s, hi, mband, mtwo})
       if (t) (void)hipStreamDestroy(t);
+  }
+  int masked(int k) {
+    if (cus == k) return JW_OK;
+    for (hipStream_t t : {mband, mtwo})
+      if (t) {
+        JW_HIP_TRY(hipStreamSynchronize(t));
+        JW_HIP_TRY(hipStreamDestroy(t));
+      }
+    int ncu = 0;
+    JW_HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    std::vector<uint32_t> a((ncu + 31) / 32, 0u), b((ncu + 31) / 32, 0u);
+    for (int i = 0; i < ncu; ++i) ((i % 8) < k ? a : b)[i / 32] |= 1u << (i % 32);
+    JW_HIP_TRY(hipExtStreamCreateWithCUMask(&mband, (uint32_t)a.size(), a.data()));
+    JW_HIP_TRY(hipExtStreamCreateWithCUMask(&mtwo, (uint32_t)b.size(), b.data()));
+    cus = k;
+    return JW_OK;
   }
 };
 static int side_stream(SideStream** out) {
@@ -735,6 +755,7 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
       st = run_fft<-1>(N, nb, in, SpecOut1{X, N, b0}, so, A, s, T, (ntm & 1) != 0);
     }
   }
+  bool band_masked = false;  // A/B runs (JW_CWT_CUS): band and two-pass on complementary CUs
   // band scales: one pass per (signal, scale) pair
   if (nband > 0 && st == JW_OK) {
     const dim3 gp((unsigned)((nb_hi * 512L + 255) / 256), (unsigned)nband);
@@ -772,8 +793,16 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
       SideStream* side = nullptr;
       if ((st = side_stream(&side)) != JW_OK) return st;
       JW_HIP_TRY(hipEventRecord(side->fork, s));
-      JW_HIP_TRY(hipStreamWaitEvent(side->s, side->fork, 0));
-      bs = side->s;
+      const char* gcu = std::getenv("JW_CWT_CUS");
+      const int k = gcu ? std::atoi(gcu) : 0;
+      if (k >= 1 && k <= 7) {
+        if ((st = side->masked(k)) != JW_OK) return st;
+        bs = side->mband;
+        band_masked = true;
+      } else {
+        bs = side->s;
+      }
+      JW_HIP_TRY(hipStreamWaitEvent(bs, side->fork, 0));
       join.side = side;  // armed before the launch: any exit below joins
     }
     auto band = [&](auto kern) {
@@ -798,7 +827,11 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   hipStream_t ps = s;
   {
     const char* gpr = std::getenv("JW_CWT_PRIO");
-    if (join.side && pairs > 0 && gpr && gpr[0] == '1') {
+    if (join.side && pairs > 0 && band_masked) {
+      JW_HIP_TRY(hipStreamWaitEvent(join.side->mtwo, join.side->fork, 0));
+      ps = join.side->mtwo;
+      join.hi = true;
+    } else if (join.side && pairs > 0 && gpr && gpr[0] == '1') {
       JW_HIP_TRY(hipStreamWaitEvent(join.side->hi, join.side->fork, 0));
       ps = join.side->hi;
       join.hi = true;
