@@ -109,14 +109,16 @@ int jw_modwt_plan_filters(const jw_modwt_plan* plan, double* g, double* h);
  * DIRECT levels are bit-identical to circularConvolve (:677-690).  FFT levels run the
  * reference's circularConvolveFFT (:752-786) with its own FFT: radix 2 with recurrence
  * twiddles for powers of two (FastFourierTransform.java:172-212) and its Bluestein transform for
- * other lengths (:259-324), both bit-identical to the JVM for 2 <= n <= 2^23 -- given that the
+ * other lengths (:259-324), both bit-identical to the JVM for power-of-two n <= 2^28 and other
+ * n <= 2^27 (transforms longer than 2^24 points run in three column passes) -- given that the
  * JVM's Math.sin/Math.cos are correctly rounded at the twiddle and chirp angles (Java specifies
  * them to 1 ulp; the engine and the oracle both take the correctly rounded value).
  * With a JW_ARITH_FMA plan (the fast contract) FFT runs the exact-twiddle frequency-domain
  * pyramid for 2 <= n <= 2^23 (within 1e-10 of DIRECT); AUTO and DIRECT run the direct kernels
  * (faster and more accurate than any FFT path on this engine).
- * A call with an FFT level (FFT, or AUTO's rule) at n > 2^23 returns JW_ERR_UNSUPPORTED naming
- * the limit (never DIRECT values in its place); DIRECT runs any n. */
+ * A call with an FFT level (FFT, or AUTO's rule) past its contract's range (STRICT: the limits
+ * above; FMA: n > 2^23) returns JW_ERR_UNSUPPORTED naming the limit (never DIRECT values in its
+ * place); DIRECT runs any n. */
 int jw_modwt_forward(const jw_modwt_plan* plan, const double* x, double* coeffs, long n,
                      int levels, int batch, int method, int where, void* stream);
 /* inverseMODWT(coefficients) (:337-375): coeffs batch x (levels+1) x n -> x batch x n.
@@ -142,7 +144,7 @@ int jw_fft_reverse(const double* in_reim, double* out_reim, long n, int batch, i
  * algorithm operation for operation -- bit reversal, radix-2 decimation in time with the
  * recurrence twiddles wn = wn.mul(w) of every stage (:172-212), Complex.mul's (ac - bd, ad + bc),
  * Bluestein for other n (:259-324) -- so results are the JVM's bit for bit for power-of-two
- * n <= 2^24 and other n <= 2^23 (correctly rounded Math.sin/cos assumed, as above); longer
+ * n <= 2^28 and other n <= 2^27 (correctly rounded Math.sin/cos assumed, as above); longer
  * STRICT lines return JW_ERR_UNSUPPORTED.  JW_ARITH_FMA is jw_fft_forward / jw_fft_reverse
  * (correctly rounded twiddle tables). */
 int jw_fft_forward_ex(const double* in_reim, double* out_reim, long n, int batch, int arith,
