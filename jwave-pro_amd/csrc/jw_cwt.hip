@@ -521,39 +521,13 @@ struct SideStream {
   int dev = -1;
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
-  // A/B runs (JW_CWT_PRIO=1): the two-pass chain on a high-priority stream beside the band
-  // kernel, so its 270 short dependent launches are dispatched ahead of the band's workgroups
-  hipStream_t hi = nullptr;
-  hipEvent_t hi_join = nullptr;
-  // A/B runs (JW_CWT_CUS=k, 1..7): the band kernel on a stream limited to k of every 8 CUs and
-  // the two-pass chain on one limited to the other 8 - k (hipExtStreamCreateWithCUMask)
-  int cus = 0;
-  hipStream_t mband = nullptr, mtwo = nullptr;
   ~SideStream() {
     if (dev < 0) return;
     (void)hipSetDevice(dev);
-    for (hipStream_t t : {s, hi, mband, mtwo})
-      if (t) (void)hipStreamSynchronize(t);
-    for (hipEvent_t e : {fork, join, hi_join})
+    if (s) (void)hipStreamSynchronize(s);
+    for (hipEvent_t e : {fork, join})
       if (e) (void)hipEventDestroy(e);
-    for (hipStream_t t : {s, hi, mband, mtwo})
-      if (t) (void)hipStreamDestroy(t);
-  }
-  int masked(int k) {
-    if (cus == k) return JW_OK;
-    for (hipStream_t t : {mband, mtwo})
-      if (t) {
-        JW_HIP_TRY(hipStreamSynchronize(t));
-        JW_HIP_TRY(hipStreamDestroy(t));
-      }
-    int ncu = 0;
-    JW_HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    std::vector<uint32_t> a((ncu + 31) / 32, 0u), b((ncu + 31) / 32, 0u);
-    for (int i = 0; i < ncu; ++i) ((i % 8) < k ? a : b)[i / 32] |= 1u << (i % 32);
-    JW_HIP_TRY(hipExtStreamCreateWithCUMask(&mband, (uint32_t)a.size(), a.data()));
-    JW_HIP_TRY(hipExtStreamCreateWithCUMask(&mtwo, (uint32_t)b.size(), b.data()));
-    cus = k;
-    return JW_OK;
+    if (s) (void)hipStreamDestroy(s);
   }
 };
 static int side_stream(SideStream** out) {
@@ -567,10 +541,6 @@ static int side_stream(SideStream** out) {
     JW_HIP_TRY(hipStreamCreateWithFlags(&ss->s, hipStreamNonBlocking));
     JW_HIP_TRY(hipEventCreateWithFlags(&ss->fork, hipEventDisableTiming));
     JW_HIP_TRY(hipEventCreateWithFlags(&ss->join, hipEventDisableTiming));
-    int least = 0, greatest = 0;
-    JW_HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    JW_HIP_TRY(hipStreamCreateWithPriority(&ss->hi, hipStreamNonBlocking, greatest));
-    JW_HIP_TRY(hipEventCreateWithFlags(&ss->hi_join, hipEventDisableTiming));
     sides[dev] = std::move(ss);
   }
   *out = sides[dev].get();
@@ -581,10 +551,8 @@ static int side_stream(SideStream** out) {
 struct JoinGuard {
   hipStream_t s = nullptr;
   SideStream* side = nullptr;
-  bool hi = false;  // the two-pass chain ran on side->hi
   ~JoinGuard() {
     if (side) (void)hipStreamWaitEvent(s, side->join, 0);
-    if (side && hi) (void)hipStreamWaitEvent(s, side->hi_join, 0);
   }
 };
 
@@ -755,7 +723,6 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
       st = run_fft<-1>(N, nb, in, SpecOut1{X, N, b0}, so, A, s, T, (ntm & 1) != 0);
     }
   }
-  bool band_masked = false;  // A/B runs (JW_CWT_CUS): band and two-pass on complementary CUs
   // band scales: one pass per (signal, scale) pair
   if (nband > 0 && st == JW_OK) {
     const dim3 gp((unsigned)((nb_hi * 512L + 255) / 256), (unsigned)nband);
@@ -793,15 +760,7 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
       SideStream* side = nullptr;
       if ((st = side_stream(&side)) != JW_OK) return st;
       JW_HIP_TRY(hipEventRecord(side->fork, s));
-      const char* gcu = std::getenv("JW_CWT_CUS");
-      const int k = gcu ? std::atoi(gcu) : 0;
-      if (k >= 1 && k <= 7) {
-        if ((st = side->masked(k)) != JW_OK) return st;
-        bs = side->mband;
-        band_masked = true;
-      } else {
-        bs = side->s;
-      }
+      bs = side->s;
       JW_HIP_TRY(hipStreamWaitEvent(bs, side->fork, 0));
       join.side = side;  // armed before the launch: any exit below joins
     }
@@ -823,20 +782,6 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     JW_HIP_TRY(hipGetLastError());
     if (join.side) JW_HIP_TRY(hipEventRecord(join.side->join, bs));
   }
-  // A/B runs: the two-pass chain on the side's high-priority stream (forked after the spectra)
-  hipStream_t ps = s;
-  {
-    const char* gpr = std::getenv("JW_CWT_PRIO");
-    if (join.side && pairs > 0 && band_masked) {
-      JW_HIP_TRY(hipStreamWaitEvent(join.side->mtwo, join.side->fork, 0));
-      ps = join.side->mtwo;
-      join.hi = true;
-    } else if (join.side && pairs > 0 && gpr && gpr[0] == '1') {
-      JW_HIP_TRY(hipStreamWaitEvent(join.side->hi, join.side->fork, 0));
-      ps = join.side->hi;
-      join.hi = true;
-    }
-  }
   // the other (signal, scale) pairs: IFFT(X * psi_hat) -> coefficients in two passes
   if (pipe && st == JW_OK) {
     auto go = [&](auto kind) {
@@ -847,7 +792,7 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
       auto mk_out = [&](long p0) {
         return CoefOut{out, n, N1, p0, 1.0 / (double)N, (ntm & 2) != 0, pmf};
       };
-      return fft::run_fft512_pipelined<1>(N, pairs, gpair, mk_in, mk_out, A, A + gpair * N, ps, T,
+      return fft::run_fft512_pipelined<1>(N, pairs, gpair, mk_in, mk_out, A, A + gpair * N, s, T,
                                           (ntm & 1) != 0);
     };
     switch (wavelet) {
@@ -858,7 +803,6 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
       default: st = go(std::integral_constant<int, JW_CWT_MEYER>{}); break;
     }
   }
-  if (join.hi) JW_HIP_TRY(hipEventRecord(join.side->hi_join, ps));
   for (long p0 = 0; p0 < pairs && st == JW_OK && !pipe; p0 += gpair) {
     const long np_ = std::min<long>(gpair, pairs - p0);
     CoefOut o{out, n, N <= 4096 ? 1 : N1, p0, 1.0 / (double)N, (ntm & 2) != 0, pmf};
