@@ -288,11 +288,6 @@ struct ColGeo {
   int rbits, cbits;
 };
 
-bool kp2p_both_filters() {
-  const char* e = std::getenv("JW_AUTO_KP2P");
-  return e && e[0] == '2';
-}
-
 // Z (nb x [C][R], forward pass-1 rows of V_{j-1}) -> Zi_h, Zi_g (inverse pass-1 rows) -> W_j,
 // and V_j either stored (last level, or a DIRECT level next) or run straight into the next
 // level's pass 1 (Z).
@@ -325,13 +320,10 @@ int forward_cols(const ModwtPlan& p, const bool* fft, const cplx* F, const cplx*
       if (st != JW_OK) break;
     }
     // forward pass 2, X . F_h / X . F_g, inverse pass 1 of each (one filter per item: a
-    // workgroup holding both products needed ~210 VGPRs, half the waves)
+    // workgroup holding both products, Z read once, needed 168 VGPRs even with the twiddle fix
+    // and ran the forward 44.0 -> 48.5 ms)
     st = with_big_lc(g.C, [&](auto LCc) -> int {
       constexpr int LC = decltype(LCc)::value;
-      if (kp2p_both_filters())  // A/B (JW_AUTO_KP2P=2): one item per signal, Z read once
-        return launch_grid<LC>(kp2p<LC, 2, RowsC, FwdMid2, OutF>, (g.R / Geo<LC>::T) * nb, s,
-                               RowsC{Z, N}, FwdMid2{spec_h(F, N, j), spec_g(F, N, j)},
-                               OutF{Zi, N, nb * N}, g.rbits, nb, twf.p2, twi.p1);
       if (FT)
         return launch_grid<LC>(kp2p<LC, 1, ZPair, FwdMidT, OutPair>, (g.R / Geo<LC>::T) * 2 * nb,
                                s, ZPair{Z, N},

@@ -211,12 +211,6 @@ struct AdjMidT {
     return jmul(x, make_double2(f.x, -f.y));
   }
 };
-// forward level, both filters per item (kp2p NF = 2): f = 0 -> h_j (W_j), 1 -> g_j (V_j)
-struct FwdMid2 {
-  const cplx* fh;
-  const cplx* fg;
-  __device__ cplx operator()(int f, long, long i, cplx x) const { return jmul(x, (f ? fg : fh)[i]); }
-};
 struct OutPair {  // item 2 sig + f -> stream f's row sig
   cplx* p;
   long st, fst;
