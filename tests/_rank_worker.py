@@ -1,5 +1,6 @@
 """One rank of the multi-process tests (started by tests/test_distributed*.py as a child
-process): joins the gloo group from RANK / WORLD_SIZE / MASTER_*, takes its contiguous shard
+process): joins the gloo group (or, --backend nccl, the RCCL communicator bench.py builds for
+N > 1) from RANK / WORLD_SIZE / MASTER_*, takes its contiguous shard
 of the global batch (jwave.distributed.shard_range, the bench's split), runs MODWT
 forward + inverse on it through the HIP C-ABI on cuda:LOCAL_RANK (or through the oracle
 with --oracle, for CPU-only runs), and all-gathers per-signal checksums in rank order.
@@ -26,13 +27,19 @@ def main():
     ap.add_argument("--items", type=int, default=11)
     ap.add_argument("--wavelet", default="Daubechies4")
     ap.add_argument("--oracle", action="store_true", help="CPU: the oracle instead of the engine")
+    ap.add_argument("--backend", default="gloo", choices=("gloo", "nccl"))
     args = ap.parse_args()
 
     import torch.distributed as dist
     from jwave import distributed as jdist
     from jwave.transforms import wavelets as W
-    rank, world = jdist.init_from_env("gloo")
-    local_rank = int(os.environ.get("LOCAL_RANK", rank))
+    local_rank = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
+    if args.backend == "nccl":  # as bench.py: the device first, then the communicator on it
+        import torch
+        torch.cuda.set_device(local_rank)
+        rank, world = jdist.init_from_env("nccl", device=torch.device("cuda", local_rank))
+    else:
+        rank, world = jdist.init_from_env("gloo")
     start, count = jdist.shard_range(args.items, rank, world)
     n, J = args.n, args.levels
     wv = W.by_name(args.wavelet)
@@ -69,7 +76,8 @@ def main():
     if rank == 0:
         print(json.dumps({"sums": [v for v in allv if v == v], "recon": recon,
                           "shards": [[int(shards[2 * r]), int(shards[2 * r + 1])]
-                                     for r in range(world)], "world": dist.get_world_size()}),
+                                     for r in range(world)], "world": dist.get_world_size(),
+                          "backend": dist.get_backend()}),
               flush=True)
     dist.destroy_process_group()
 
