@@ -240,11 +240,31 @@ __device__ __forceinline__ d2 rev_pair_rot(const double* buf, int h, int u, cons
   return d2{a0, a1};
 }
 
+// Level barrier of the line cascades: workgroup-wide, or (WS) wave-level when every line's
+// threads sit in one wavefront (NTL divides 64), whose DS instructions execute in issue order
+// -- a wave-scope fence pair around a wave barrier keeps the compiler from moving LDS accesses
+// across it.
+#ifndef JW_TAIL_WSYNC  // A/B builds: 0 = workgroup barriers in the column tails too
+#define JW_TAIL_WSYNC 1
+#endif
+template <bool WS>
+__device__ __forceinline__ void line_sync() {
+  if constexpr (WS) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
+}
+
 // The forward cascade on one line held in LDS (buf), by NTL threads (tid < NTL).  The
-// barriers are workgroup-wide: every line of the workgroup runs the same levels.
-template <bool FMA, int M, int NTL, int LEN = kLdsN>
+// barriers are workgroup-wide (every line of the workgroup runs the same levels), or wave-level
+// with WS.
+template <bool FMA, int M, int NTL, int LEN = kLdsN, bool WS = false>
 __device__ __forceinline__ void cascade_fwd(double* buf, int n, int level, int tw, int tid,
                                             const Filters& f) {
+  static_assert(!WS || (NTL <= 64 && 64 % NTL == 0), "wave-level syncs: one line per wave part");
   constexpr int P = (LEN / NTL / 2) < 1 ? 1 : LEN / NTL / 2;  // pairs per thread, first level
   int l = 0;
   for (int h = n; h >= tw && h >= 2 && l < level; h >>= 1, ++l) {
@@ -267,7 +287,7 @@ __device__ __forceinline__ void cascade_fwd(double* buf, int n, int level, int t
       }
       if (i + NTL >= half) break;
     }
-    __syncthreads();
+    line_sync<WS>();
 #pragma unroll
     for (int r = 0; r < P; ++r) {
       const int i = tid + r * NTL;
@@ -276,7 +296,7 @@ __device__ __forceinline__ void cascade_fwd(double* buf, int n, int level, int t
         buf[i + half] = hi[r];
       }
     }
-    __syncthreads();
+    line_sync<WS>();
   }
 }
 
@@ -294,10 +314,11 @@ __global__ __launch_bounds__(kNT2) void fwt_fwd_lds2(const double* __restrict__ 
   for (int i = 2 * tid; i < n; i += 2 * kNT2) *(d2*)&ys[i] = *(const d2*)&buf[i];
 }
 
-template <bool FMA, int M, int KIND, int NTL, int LEN = kLdsN>
+template <bool FMA, int M, int KIND, int NTL, int LEN = kLdsN, bool WS = false>
 __device__ __forceinline__ void cascade_rev(double* buf, int n, int h0, int tw, int tid,
                                             const Filters& f, const d2* tp,
                                             double* gout = nullptr) {
+  static_assert(!WS || (NTL <= 64 && 64 % NTL == 0), "wave-level syncs: one line per wave part");
   constexpr int P = (LEN / NTL / 2) < 1 ? 1 : LEN / NTL / 2;
   for (int h = h0; h <= n && h >= tw && h >= 2; h <<= 1) {
     const int half = h >> 1;
@@ -343,13 +364,13 @@ __device__ __forceinline__ void cascade_rev(double* buf, int n, int h0, int tw, 
       }
       return;
     }
-    __syncthreads();
+    line_sync<WS>();
 #pragma unroll
     for (int r = 0; r < P; ++r) {
       const int u = tid + r * NTL;
       if (u < half) *(d2*)&buf[2 * u] = o[r];
     }
-    __syncthreads();
+    line_sync<WS>();
   }
 }
 
@@ -1068,11 +1089,16 @@ __global__ __launch_bounds__(kTailNT) void fwt_cols_tail(const double* in, doubl
   }
   __syncthreads();
   double* buf = bufs + g * PAD;
+  // each column's NTL = 32 threads are half a wavefront: its levels sync at wave level, and
+  // only the loads and stores across columns take workgroup barriers (cfg4 -0.5..-1 %,
+  // profiles/r04/ab/fwt_tail_wsync_j.log)
+  constexpr bool WS = JW_TAIL_WSYNC != 0;
   if (REV) {
-    cascade_rev<FMA, M, KIND, NTL, kTailLen>(buf, len, lvl_h0, tw, lt, f, tp);
+    cascade_rev<FMA, M, KIND, NTL, kTailLen, WS>(buf, len, lvl_h0, tw, lt, f, tp);
   } else {
-    cascade_fwd<FMA, M, NTL, kTailLen>(buf, len, lvl_h0, tw, lt, f);
+    cascade_fwd<FMA, M, NTL, kTailLen, WS>(buf, len, lvl_h0, tw, lt, f);
   }
+  if (WS) __syncthreads();  // the stores below read other waves' columns
   for (int k = tid; k < len * kTailNL; k += kTailNT) {
     const int i = k / kTailNL, c = k % kTailNL;
     dst[(long)i * cols + c] = bufs[c * PAD + i];
