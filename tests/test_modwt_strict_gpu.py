@@ -254,13 +254,26 @@ def test_modwt_long_lines_bit_exact(wname, n, J, threshold, method, monkeypatch)
         assert bits_equal(xr[b], orc.modwt_inverse(ref, g, h, method, threshold)), b
 
 
-def test_fft_strict_2_25():
-    # the smallest length past the two-pass split, with the default (three-pass) geometry
-    n = 1 << 25
-    rng = np.random.default_rng(25)
+@pytest.mark.parametrize("lg", [25, 26, 27])
+def test_fft_strict_three_pass_default_geometry(lg):
+    # past the two-pass split, with the default geometry (jw_jfft_host.hpp split3: 2^12 x 2^6 x
+    # 2^(lg - 18)); the oracle takes ~6 / 13 / 28 s for these on one core
+    n = 1 << lg
+    rng = np.random.default_rng(lg)
     z = rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n)
     X = FastFourierTransform().forwardComplex(z)
     assert bits_equal(X.view(np.float64), orc.fft(z).view(np.float64))
+
+
+def test_auto_2_25_forward_bit_exact():
+    # JWave's default path at a length past the two-pass FFT: db4 level 1 through the
+    # unfused long-line MODWT (jw_jfft.hip modwt_strict_long) on three-pass transforms
+    n = 1 << 25
+    wv = W.Daubechies4()
+    g, h = ofilters(wv)
+    x = orc.fill_uniform(n, 25)
+    c = MODWTTransform(wv).forwardMODWT(x[None, :], 1)
+    assert bits_equal(c[0], orc.modwt_forward(x, 1, g, h, "auto"))
 
 
 @pytest.mark.parametrize("n", [70001, 200001])
