@@ -33,7 +33,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "modwt_pmc_traffic.json")
 # cwt / fwt2d HBM bytes per step at their default configs (tools/pmc_traffic.sh,
 # tools/traffic_summary.py)
-TRAFFIC_STEP_FILE = os.path.join(ROOT, "profiles", "r03", "final_d", "traffic_cwt_fwt2d.json")
+TRAFFIC_STEP_FILE = os.path.join(ROOT, "profiles", "r04", "final_f", "traffic_cwt_fwt2d.json")
 
 
 def generate_inputs(gen, min_seconds=1.0):
@@ -288,9 +288,11 @@ def main_cwt(args, dev, rank, world):
                          "algorithmic_bytes_per_launch": per_call,
                          "note": "one launch = one jw_cwt_fft call over the batch (all FFT "
                                  "passes); traffic = rocprofv3 FETCH_SIZE*2 + WRITE_SIZE per call "
-                                 "(profiles/r03/final_d/traffic_cwt_fwt2d.json): the A workspace round "
+                                 "(profiles/r04/final_f/traffic_cwt_fwt2d.json): the A workspace round "
                                  "trip of the two-pass scales is the excess over algorithmic; the "
-                                 "band scales (cwt_band512) run in one pass"},
+                                 "band scales (cwt_band512) run in one pass.  The structure's own "
+                                 "floor (34 two-pass scales at 3x their output, 30 one-pass) is "
+                                 "~142 GB per call (DESIGN.md 9c)"},
             "cpu_baseline": cpu}), flush=True)
 
 
