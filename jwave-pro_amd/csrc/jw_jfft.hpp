@@ -49,8 +49,8 @@ __host__ __device__ constexpr int ilog2(long v) {
 #ifndef JF_EPT1024
 #define JF_EPT1024 8
 #endif
-#ifndef JF_PSH
-#define JF_PSH 4
+#ifndef JF_PSH  // LDS padding: one slot per 2^JF_PSH points (A/B builds: 4)
+#define JF_PSH 3
 #endif
 template <int LC>
 struct Geo {
@@ -61,8 +61,8 @@ struct Geo {
   static constexpr int GMAX = ilog2(EPT);
   static constexpr int TPC = LC / EPT;  // threads per column (divides 64 when <= 64)
   static constexpr int T = kNT / TPC;   // columns per workgroup
-  // padded column stride: one slot per 2^JF_PSH points (JF_PSH 3 and a tuned tail for the
-  // register-I/O layout, A/B builds), one per column
+  // padded column stride: one slot per 8 points and a tail per length (AUTO STRICT +1.5 %
+  // over one per 16, profiles/r04/ab/auto_regio8_pad8_n.log); JF_PSH=4 restores that layout
   static constexpr int CS = JF_PSH == 3 ? LC + LC / 8 + (LC == 1024 ? 3 : LC == 2048 ? 5 : 1)
                                         : LC + LC / 16 + 1;
   static constexpr size_t LDS_BYTES = (size_t)T * CS * sizeof(cplx);
@@ -246,73 +246,6 @@ __device__ __forceinline__ void store_cols(const cplx* lds, const Out& out, long
   }
 }
 
-#ifndef JF_REGIO
-#define JF_REGIO 0
-#endif
-// Register I/O (JF_REGIO): a column kernel's first stage group runs on its points as they
-// arrive from global memory, and its last group hands its points straight to the stores, so a
-// column pass makes two LDS round trips fewer (3 writes per point instead of 5 for 1024
-// points).  The I/O phases map threads to columns interleaved (column tid % T, set tid / T):
-// a wave's load or store covers 16 rows x T columns, the same pieces as load_cols/store_cols.
-// The butterflies and their order are unchanged (bit-identical).
-template <int LC>
-struct RIO {
-  using G = Geo<LC>;
-  static_assert(G::EPT == 8 && G::GMAX == 3, "register I/O: radix-8 groups of 8 points");
-  static constexpr int T0L = ((G::LOG - 1) / G::GMAX) * G::GMAX;  // the last group's first stage
-  static constexpr int GL = G::LOG - T0L;
-  static constexpr int EL = 1 << GL, NSL = G::EPT / EL;
-  static_assert(T0L >= 3, "register I/O: two groups at least");
-  // the last group's point idx (set i, member m) sits at own_pos k = i + NSL m
-  static constexpr int k_of(int idx) { return idx / EL + NSL * (idx % EL); }
-  static constexpr int rev3(int k) { return ((k & 1) << 2) | (k & 2) | ((k >> 2) & 1); }
-  __device__ static int cc() { return threadIdx.x % G::T; }
-  __device__ static int tl() { return threadIdx.x / G::T; }
-  __device__ static int pos_last(int tl, int idx) { return tl + G::TPC * k_of(idx); }
-};
-
-// group 1 (stages 0..2) of set s in registers (positions 8 s + m), then into the column
-template <int LC>
-__device__ __forceinline__ void rio_first(cplx (&v)[8], cplx* __restrict__ col, int s,
-                                          const cplx* __restrict__ tw) {
-  const int base[1] = {8 * s};
-  stage_math<LC, 3>(v, base, 0, tw);
-#pragma unroll
-  for (int m = 0; m < 8; ++m) col[pidx(8 * s + m)] = v[m];
-}
-
-// the last group of I/O thread tl, out of the column into registers (v[idx] at pos_last)
-template <int LC>
-__device__ __forceinline__ void rio_last(cplx (&v)[8], const cplx* __restrict__ col, int tl,
-                                         const cplx* __restrict__ tw) {
-  using R = RIO<LC>;
-  int base[R::NSL];
-#pragma unroll
-  for (int i = 0; i < R::NSL; ++i) {
-    base[i] = set_base(tl + Geo<LC>::TPC * i, R::T0L, R::GL);
-#pragma unroll
-    for (int m = 0; m < R::EL; ++m) v[i * R::EL + m] = col[pidx(base[i] + (m << R::T0L))];
-  }
-  stage_math<LC, R::GL>(v, base, R::T0L, tw);
-}
-
-// One column pass in register-I/O form: v holds set s's points on entry, the I/O thread's
-// last-group points on return.  twio / twmid: the twiddles of the I/O thread's column and of
-// the middle-phase thread's column (one table for every column in a pass 1).  The caller
-// makes sure no thread still reads the LDS tile when it enters.
-template <int LC>
-__device__ __forceinline__ void rio_pass(cplx (&v)[8], cplx* __restrict__ lds, int s,
-                                         const cplx* __restrict__ twio,
-                                         const cplx* __restrict__ twmid) {
-  using G = Geo<LC>;
-  using R = RIO<LC>;
-  rio_first<LC>(v, lds + R::cc() * G::CS, s, twio);
-  __syncthreads();
-  run_stages<LC, 3, R::T0L>(lds + (threadIdx.x / G::TPC) * G::CS, threadIdx.x % G::TPC, twmid);
-  __syncthreads();
-  rio_last<LC>(v, lds + R::cc() * G::CS, R::tl(), twio);
-}
-
 // pass 1: columns of [LC][W] (bit-reversed into LDS), stages with the natural table, rows of Z
 template <int LC, class In, class Out>
 __global__ __launch_bounds__(kNT) void kp1(In in, Out out, int wbits, long nitems,
@@ -323,19 +256,6 @@ __global__ __launch_bounds__(kNT) void kp1(In in, Out out, int wbits, long nitem
   long item;
   tile_item((1 << wbits) / G::T, nitems, &tile, &item);
   const int c0 = tile * G::T;
-  if constexpr (JF_REGIO) {
-    using R = RIO<LC>;
-    const int cio = R::cc(), s = R::tl();
-    cplx v[8];
-#pragma unroll
-    for (int m = 0; m < 8; ++m)
-      v[m] = in(item, ((long)brev(8 * s + m, G::LOG) << wbits) + c0 + cio);
-    rio_pass<LC>(v, lds, s, tw1, tw1);
-    const long row = (long)brev(c0 + cio, wbits) * LC;
-#pragma unroll
-    for (int idx = 0; idx < 8; ++idx) out(item, row + R::pos_last(s, idx), v[idx]);
-    return;
-  }
   load_cols<LC, true>(lds, in, item, c0, wbits);
   __syncthreads();
   const int cc = threadIdx.x / G::TPC, tl = threadIdx.x % G::TPC;
@@ -354,19 +274,6 @@ __global__ __launch_bounds__(kNT) void kp2s(In in, Out out, int wbits, long nite
   long item;
   tile_item((1 << wbits) / G::T, nitems, &tile, &item);
   const int c0 = tile * G::T;
-  if constexpr (JF_REGIO) {
-    using R = RIO<LC>;
-    const int cio = R::cc(), s = R::tl();
-    cplx v[8];
-#pragma unroll
-    for (int m = 0; m < 8; ++m) v[m] = in(item, ((long)(8 * s + m) << wbits) + c0 + cio);
-    rio_pass<LC>(v, lds, s, tw2 + (long)(c0 + cio) * LC,
-                 tw2 + (long)(c0 + threadIdx.x / G::TPC) * LC);
-#pragma unroll
-    for (int idx = 0; idx < 8; ++idx)
-      out(item, ((long)R::pos_last(s, idx) << wbits) + c0 + cio, v[idx]);
-    return;
-  }
   load_cols<LC, false>(lds, in, item, c0, wbits);
   __syncthreads();
   const int cc = threadIdx.x / G::TPC, tl = threadIdx.x % G::TPC;
@@ -396,34 +303,6 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(NF == 1 ? J
   long item;
   tile_item((1 << wbits) / G::T, nitems, &tile, &item);
   const int c0 = tile * G::T;
-  if constexpr (JF_REGIO) {
-    using R = RIO<LC>;
-    const int cio = R::cc(), s = R::tl();
-    const long lio = c0 + cio;
-    cplx X[8];
-#pragma unroll
-    for (int m = 0; m < 8; ++m) X[m] = in(item, ((long)(8 * s + m) << wbits) + lio);
-    rio_pass<LC>(X, lds, s, tw2 + lio * LC, tw2 + (long)(c0 + threadIdx.x / G::TPC) * LC);
-    const long row = (long)brev(c0 + cio, wbits) * LC;
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      // point h = pos_last(s, idx) goes to position brev(h) = rev3(k) + 8 brev(s) of the next
-      // transform's column: set brev(s), member rev3(k)
-      cplx u[8];
-#pragma unroll
-      for (int idx = 0; idx < 8; ++idx) {
-        const long h = R::pos_last(s, idx);
-        u[R::rev3(R::k_of(idx))] = mid(f, item, (h << wbits) + lio, X[idx]);
-      }
-      const cplx* tw1f = tw1;
-      if (NF > 1) asm volatile("" : "+v"(tw1f));
-      __syncthreads();  // every read of the tile (the last group before) is done
-      rio_pass<LC>(u, lds, brev(s, G::LOG - 3), tw1f, tw1f);
-#pragma unroll
-      for (int idx = 0; idx < 8; ++idx) out(f, item, row + R::pos_last(s, idx), u[idx]);
-    }
-    return;
-  }
   load_cols<LC, false>(lds, in, item, c0, wbits);
   __syncthreads();
   const int cc = threadIdx.x / G::TPC, tl = threadIdx.x % G::TPC;
@@ -478,44 +357,6 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(
   long item;
   tile_item((1 << wbits) / G::T, nitems, &tile, &item);
   const int c0 = tile * G::T;
-  if constexpr (JF_REGIO) {
-    using R = RIO<LC>;
-    const int cio = R::cc(), s = R::tl();
-    const long lio = c0 + cio;
-    double acc[8];
-#pragma unroll
-    for (int si = 0; si < NIN; ++si) {
-      if (si > 0) __syncthreads();  // every read of the tile by the previous input is done
-      cplx v[8];
-#pragma unroll
-      for (int m = 0; m < 8; ++m) v[m] = in(si, item, ((long)(8 * s + m) << wbits) + lio);
-      const cplx* tws = tw2 + lio * LC;
-      const cplx* twm = tw2 + (long)(c0 + threadIdx.x / G::TPC) * LC;
-      if (NIN > 1) asm volatile("" : "+v"(tws), "+v"(twm));
-      rio_pass<LC>(v, lds, s, tws, twm);
-#pragma unroll
-      for (int idx = 0; idx < 8; ++idx) {
-        const long h = R::pos_last(s, idx);
-        const double pv = post(si, item, (h << wbits) + lio, v[idx]);
-        acc[idx] = si == 0 ? pv : acc[idx] + pv;
-      }
-    }
-    if constexpr (FUSE) {
-      cplx u[8];
-#pragma unroll
-      for (int idx = 0; idx < 8; ++idx) u[R::rev3(R::k_of(idx))] = make_double2(acc[idx], 0.0);
-      __syncthreads();
-      rio_pass<LC>(u, lds, brev(s, G::LOG - 3), tw1f, tw1f);
-      const long row = (long)brev(c0 + cio, wbits) * LC;
-#pragma unroll
-      for (int idx = 0; idx < 8; ++idx) out(item, row + R::pos_last(s, idx), u[idx]);
-    } else {
-#pragma unroll
-      for (int idx = 0; idx < 8; ++idx)
-        out(item, ((long)R::pos_last(s, idx) << wbits) + lio, acc[idx]);
-    }
-    return;
-  }
   const int cc = threadIdx.x / G::TPC, tl = threadIdx.x % G::TPC;
   cplx* col = lds + cc * G::CS;
   const long l = c0 + cc;
