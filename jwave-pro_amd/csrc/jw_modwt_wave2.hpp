@@ -179,7 +179,15 @@ struct HP : HistP<L, J, JL> {
 // launch picks it when (J + 1) N 8 < 2^31) instead of one resource per row: 4 SGPRs instead of
 // 4 (J + 1), which for sym8 J=6 cuts the SGPR spills (to VGPR lanes, read back per tap use)
 // from 92 to 18.
-template <int L, int J, bool FMA, int D, int U, int MEM = 1, bool ONE = false>
+// ROT: the register rings whose length divides a trip's sub-steps rotate by index instead of
+// shifting (sym8 J=6: no ring moves, 4 steps per trip; db4 J=8: the same instructions in another
+// register assignment).  cfg2 inverse 16.82 -> 15.96-16.00 ms, cfg5 16.10 -> 15.90 ms on one box
+// (profiles/r04/ab/inv_rot_o.log); JW_INV2_ROT=0 builds the shifting form.
+#ifndef JW_INV2_ROT
+#define JW_INV2_ROT 1
+#endif
+template <int L, int J, bool FMA, int D, int U, int MEM = 1, bool ONE = false,
+          bool ROT = JW_INV2_ROT != 0>
 __global__ __launch_bounds__(64) void modwt_inv_wave2(const double* __restrict__ coeffs,
                                                       double* __restrict__ x, long N, long seg_len,
                                                       long a_start, long ngroups, Taps taps) {
@@ -269,32 +277,46 @@ __global__ __launch_bounds__(64) void modwt_inv_wave2(const double* __restrict__
         // register levels J .. 7 and level 6 for sub-steps e = 1 (a + 64 + l), then e = 0
 #pragma unroll
         for (int e = 1; e >= 0; --e) {
+          // ROT: a ring whose length divides the trip's 2U sub-steps is rotated by index (its
+          // newest entry at (k - c) mod length in sub-step c of the trip) instead of shifted
+          const int c = 2 * u + (1 - e);
           double vv = cur.r[J - 5][e];  // V_J
 #pragma unroll
           for (int j = J; j > 6; --j) {
-            const int ro = GW::roff(j), q = GW::q(j);
+            const int ro = GW::roff(j), q = GW::q(j), R = GW::ring(j);
+            const bool rot = ROT && (2 * U) % R == 0;
+            auto ri = [&](int k) { return ro + (rot ? ((k - c) % R + R) % R : k); };
+            if (!rot) {
 #pragma unroll
-            for (int k = GW::ring(j) - 1; k >= 1; --k) rg[ro + k] = rg[ro + k - 1];
-            rg[ro] = d2{vv, cur.r[j - 6][e]};
+              for (int k = R - 1; k >= 1; --k) rg[ro + k] = rg[ro + k - 1];
+            }
+            rg[ri(0)] = d2{vv, cur.r[j - 6][e]};
             double ap = 0.0, dp = 0.0;
 #pragma unroll
             for (int m = 0; m < L; ++m) {
-              ap = madd<FMA>(ap, taps.a[m], rg[ro + m * q].x);
-              dp = madd<FMA>(dp, taps.b[m], rg[ro + m * q].y);
+              ap = madd<FMA>(ap, taps.a[m], rg[ri(m * q)].x);
+              dp = madd<FMA>(dp, taps.b[m], rg[ri(m * q)].y);
             }
             vv = ap + dp;  // V_{j-1}
           }
+          constexpr bool RX = ROT && (2 * U) % GW::NX == 0 && (2 * U) % GW::NZ == 0;
+          auto xi = [&](int k) { return RX ? ((k - c) % GW::NX + GW::NX) % GW::NX : k; };
+          auto zi = [&](int k) { return RX ? ((k - c) % GW::NZ + GW::NZ) % GW::NZ : k; };
+          if (!RX) {
 #pragma unroll
-          for (int k = GW::NX - 1; k >= 1; --k) xr[k] = xr[k - 1];
-          xr[0] = d2{vv, cur.r[0][e]};
-          const d2 z = partner32(xr[0], xr[1], lane);
+            for (int k = GW::NX - 1; k >= 1; --k) xr[k] = xr[k - 1];
+          }
+          xr[xi(0)] = d2{vv, cur.r[0][e]};
+          const d2 z = partner32(xr[xi(0)], xr[xi(1)], lane);
+          if (!RX) {
 #pragma unroll
-          for (int k = GW::NZ - 1; k >= 1; --k) zr[k] = zr[k - 1];
-          zr[0] = z;
+            for (int k = GW::NZ - 1; k >= 1; --k) zr[k] = zr[k - 1];
+          }
+          zr[zi(0)] = z;
           double ap = 0.0, dp = 0.0;
 #pragma unroll
           for (int m = 0; m < L; ++m) {
-            const d2 t = (m & 1) ? zr[m >> 1] : xr[m >> 1];
+            const d2 t = (m & 1) ? zr[zi(m >> 1)] : xr[xi(m >> 1)];
             ap = madd<FMA>(ap, taps.a[m], t.x);
             dp = madd<FMA>(dp, taps.b[m], t.y);
           }
@@ -331,7 +353,9 @@ constexpr bool inv_prefer2() {
   return J <= 7 || L <= 8;
 }
 
-template <int L, int J, bool FMA, int D = 2, int U = 2>
+// steps per loop trip: 2, or 4 for 16 taps with ROT (the level-6 rings of 8 entries then rotate
+// once per trip; at 8 taps they are 4 long and U = 2 suffices)
+template <int L, int J, bool FMA, int D = 2, int U = (JW_INV2_ROT && L == 16) ? 4 : 2>
 int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hipStream_t s) {
   using G = G2<L, J>;
   const long warm = ((long)(G::H + kS - 1) / kS) * kS;
