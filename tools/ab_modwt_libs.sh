@@ -7,12 +7,12 @@ cd "$R" || exit 2
 O="gpurun_out/ab_modwt_libs_$1"; shift; mkdir -p "$O"
 LIBS=("libjwave_hip.so")
 for n in "$@"; do LIBS+=("ab/libjwave_hip_$n.so"); done
-for rep in 1 2; do
+for rep in ${REPS:-1 2}; do
   for lib in "${LIBS[@]}"; do
     for w in "Daubechies4 8" "Symlet8 6"; do
       read -r wn wl <<< "$w"
       JWAVE_HIP_LIB=$R/jwave-pro_amd/$lib timeout -k 10 300 python3 bench.py --wavelet $wn \
-        --levels $wl --steps 5 --warmup 2 --no-cpu-baseline --no-check > "$O/one.log" 2>&1 \
+        --levels $wl --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline --no-check > "$O/one.log" 2>&1 \
         || { echo "$lib failed"; tail -5 "$O/one.log"; exit 1; }
       python3 -c "
 import json
