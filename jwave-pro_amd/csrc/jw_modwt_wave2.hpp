@@ -180,9 +180,9 @@ struct HP : HistP<L, J, JL> {
 // 4 (J + 1), which for sym8 J=6 cuts the SGPR spills (to VGPR lanes, read back per tap use)
 // from 92 to 18.
 // ROT: the register rings whose length divides a trip's sub-steps rotate by index instead of
-// shifting (sym8 J=6: no ring moves, 4 steps per trip; db4 J=8: the same instructions in another
-// register assignment).  cfg2 inverse 16.82 -> 15.96-16.00 ms, cfg5 16.10 -> 15.90 ms on one box
-// (profiles/r04/ab/inv_rot_o.log); JW_INV2_ROT=0 builds the shifting form.
+// shifting (sym8 J=6: no ring moves, 4 steps per trip; db4 J=8: the compiler renamed them
+// already).  cfg5 inverse 15.86-15.91 -> 15.69-15.71 ms, cfg2 unchanged, on one box
+// (profiles/r04/ab/inv_rot_q.log); JW_INV2_ROT=0 builds the shifting form.
 #ifndef JW_INV2_ROT
 #define JW_INV2_ROT 1
 #endif
