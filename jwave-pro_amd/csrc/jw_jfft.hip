@@ -526,6 +526,14 @@ int modwt_strict(bool inverse, const ModwtPlan& p, const double* in, double* out
   ColGeo g;
   g.N = N;
   g.R = split_lc1(N);
+  {
+    // A/B runs: JW_AUTO_R = the forward pass-1 column length (a power of two, 64 .. 4096,
+    // with N / R in the same range); the split changes no operation, only the access shapes
+    const char* e = std::getenv("JW_AUTO_R");
+    const long r = e ? std::atol(e) : 0;
+    if (r >= 64 && r <= 4096 && (r & (r - 1)) == 0 && N % r == 0 && N / r >= 64 && N / r <= 4096)
+      g.R = r;
+  }
   g.C = N / g.R;
   g.rbits = ilog2(g.R);
   g.cbits = ilog2(g.C);
