@@ -526,9 +526,15 @@ int modwt_strict(bool inverse, const ModwtPlan& p, const double* in, double* out
   ColGeo g;
   g.N = N;
   g.R = split_lc1(N);
+  // The inverse levels run faster with the shorter pass-1 columns (more columns per kp1 / kp2r
+  // workgroup: 128-byte pieces) and longer kp2p columns: at N = 2^20, 512 x 2048 instead of
+  // 1024 x 1024 took the db4 J=8 inverse 50.6 -> 49.5 ms and the sym8 J=6 one 38.1 -> 37.2 ms per
+  // 128 signals, while the forward prefers the square split (profiles/r04/ab/auto_split_r.log).
+  // Bit-identical either way (the split changes no operation, only the access shapes).
+  if (inverse && g.R >= 1024 && N / (g.R / 2) <= 2048) g.R /= 2;
   {
     // A/B runs: JW_AUTO_R = the forward pass-1 column length (a power of two, 64 .. 4096,
-    // with N / R in the same range); the split changes no operation, only the access shapes
+    // with N / R in the same range)
     const char* e = std::getenv("JW_AUTO_R");
     const long r = e ? std::atol(e) : 0;
     if (r >= 64 && r <= 4096 && (r & (r - 1)) == 0 && N % r == 0 && N / r >= 64 && N / r <= 4096)
