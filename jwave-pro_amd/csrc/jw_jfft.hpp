@@ -24,7 +24,7 @@
 // column read consecutive entries.  Short transforms (n <= 4096) run whole in one "column".
 //
 // A column of LC points is held by LC/EPT threads with EPT = min(8, LC) points each; a
-// workgroup of 512 threads holds T = 512 EPT / LC columns in LDS (padded: one slot per 16
+// workgroup of 512 threads holds T = 512 EPT / LC columns in LDS (padded: one slot per 8
 // points, one per column).  Stages run in register groups of up to 3 (radix 8): at <= 128
 // VGPRs four waves per SIMD stay resident (16 points per thread needed ~200).
 #pragma once
