@@ -12,7 +12,7 @@ for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if not any(s in k for s in ("modwt", "fwt", "cwt", "inv_nomem", "pass512", "pass_generic", "psi_table")):
+        if not any(s in k for s in ("modwt", "fwt", "cwt", "inv_nomem", "pass512", "pass_generic", "psi_table", "jf::kp")):
             continue
         k = k.replace("(anonymous namespace)", "anon").split("(")[0].replace("void ", "")[:90]
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
