@@ -49,8 +49,8 @@ __host__ __device__ constexpr int ilog2(long v) {
 #ifndef JF_EPT1024
 #define JF_EPT1024 8
 #endif
-#ifndef JF_PSH  // LDS padding: one slot per 2^JF_PSH points (A/B builds: 4)
-#define JF_PSH 3
+#ifndef JF_SWZ  // LDS layout of a column (A/B builds: 0 = one pad slot per 8 points)
+#define JF_SWZ 1
 #endif
 template <int LC>
 struct Geo {
@@ -61,14 +61,27 @@ struct Geo {
   static constexpr int GMAX = ilog2(EPT);
   static constexpr int TPC = LC / EPT;  // threads per column (divides 64 when <= 64)
   static constexpr int T = kNT / TPC;   // columns per workgroup
-  // padded column stride: one slot per 8 points and a tail per length (AUTO STRICT +1.5 %
-  // over one per 16, profiles/r04/ab/auto_regio8_pad8_n.log); JF_PSH=4 restores that layout
-  static constexpr int CS = JF_PSH == 3 ? LC + LC / 8 + (LC == 1024 ? 3 : LC == 2048 ? 5 : 1)
-                                        : LC + LC / 16 + 1;
+  // column stride: the XOR-swizzled layout (pidx) needs no padding inside a column, 6 slots
+  // between columns; the padded one (short columns, JF_SWZ=0) one slot per 8 points
+  static constexpr bool SWZ = JF_SWZ && LC >= 128;
+  static constexpr int CS = SWZ ? LC + 6 : LC + LC / 8 + (LC == 1024 ? 3 : LC == 2048 ? 5 : 1);
   static constexpr size_t LDS_BYTES = (size_t)T * CS * sizeof(cplx);
 };
 
-__device__ __forceinline__ int pidx(int pos) { return pos + (pos >> JF_PSH); }
+// LDS slot of column position pos.  Columns of >= 128 points: the low three bits XORed with bits
+// 3-5, 6-8 and 9-11 (a permutation inside each group of 8 slots), which spreads the strided
+// and bit-reversed accesses of the stage groups, the staging and the kp2p / kp2r transitions
+// over the banks (a bank model of those phases: 9,984 vs 18,944 conflict-weighted group
+// cycles for 1024 points with the 8-point padding; the bit-reversed transition writes were
+// 8-way conflicts); shorter columns keep one pad slot per 8 points.
+template <int LC>
+__device__ __forceinline__ int pidx(int pos) {
+  if constexpr (Geo<LC>::SWZ) {
+    return pos ^ ((pos >> 3) & 7) ^ ((pos >> 6) & 7) ^ ((pos >> 9) & 7);
+  } else {
+    return pos + (pos >> 3);
+  }
+}
 __device__ __forceinline__ int brev(int v, int bits) {
   return bits == 0 ? 0 : (int)(__builtin_bitreverse32((unsigned)v) >> (32 - bits));
 }
@@ -143,13 +156,13 @@ __device__ __forceinline__ void stage_group(cplx* __restrict__ col, int tl, int 
   for (int i = 0; i < NSET; ++i) {
     base[i] = set_base(tl + Gm::TPC * i, t0, G);
 #pragma unroll
-    for (int m = 0; m < E; ++m) v[i * E + m] = col[pidx(base[i] + (m << t0))];
+    for (int m = 0; m < E; ++m) v[i * E + m] = col[pidx<LC>(base[i] + (m << t0))];
   }
   stage_math<LC, G>(v, base, t0, tw);
 #pragma unroll
   for (int i = 0; i < NSET; ++i) {
 #pragma unroll
-    for (int m = 0; m < E; ++m) col[pidx(base[i] + (m << t0))] = v[i * E + m];
+    for (int m = 0; m < E; ++m) col[pidx<LC>(base[i] + (m << t0))] = v[i * E + m];
   }
 }
 
@@ -218,7 +231,7 @@ __device__ __forceinline__ void load_cols(cplx* lds, const In& in, long item, in
   for (int k = 0; k < G::EPT; ++k) {
     const int f = threadIdx.x + kNT * k;
     const int r = f / G::T;
-    lds[(f % G::T) * G::CS + pidx(REV ? brev(r, G::LOG) : r)] = v[k];
+    lds[(f % G::T) * G::CS + pidx<LC>(REV ? brev(r, G::LOG) : r)] = v[k];
   }
 }
 
@@ -230,7 +243,7 @@ __device__ __forceinline__ void store_rows(const cplx* lds, const Out& out, long
   for (int k = 0; k < G::EPT; ++k) {
     const int f = threadIdx.x + kNT * k;
     const int cc = f / LC, pos = f % LC;
-    out(item, (long)brev(c0 + cc, wbits) * LC + pos, lds[cc * G::CS + pidx(pos)]);
+    out(item, (long)brev(c0 + cc, wbits) * LC + pos, lds[cc * G::CS + pidx<LC>(pos)]);
   }
 }
 
@@ -242,7 +255,7 @@ __device__ __forceinline__ void store_cols(const cplx* lds, const Out& out, long
   for (int k = 0; k < G::EPT; ++k) {
     const int f = threadIdx.x + kNT * k;
     const int cc = f % G::T, r = f / G::T;
-    out(item, ((long)r << wbits) + c0 + cc, lds[cc * G::CS + pidx(r)]);
+    out(item, ((long)r << wbits) + c0 + cc, lds[cc * G::CS + pidx<LC>(r)]);
   }
 }
 
@@ -311,7 +324,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(NF == 1 ? J
   col_sync<LC>();
   cplx X[G::EPT];
 #pragma unroll
-  for (int k = 0; k < G::EPT; ++k) X[k] = col[pidx(own_pos<LC>(tl, k))];
+  for (int k = 0; k < G::EPT; ++k) X[k] = col[pidx<LC>(own_pos<LC>(tl, k))];
   const long l = c0 + cc;
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
@@ -323,7 +336,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(NF == 1 ? J
 #pragma unroll
     for (int k = 0; k < G::EPT; ++k) {
       const int h = own_pos<LC>(tl, k);
-      col[pidx(brev(h, G::LOG))] = mid(f, item, ((long)h << wbits) + l, X[k]);
+      col[pidx<LC>(brev(h, G::LOG))] = mid(f, item, ((long)h << wbits) + l, X[k]);
     }
     col_sync<LC>();
     // every product runs the same pass-1 twiddles: opaque per product, or the compiler holds
@@ -376,7 +389,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
     for (int k = 0; k < G::EPT; ++k) {
       const int h = own_pos<LC>(tl, k);
-      const double v = post(s, item, ((long)h << wbits) + l, col[pidx(h)]);
+      const double v = post(s, item, ((long)h << wbits) + l, col[pidx<LC>(h)]);
       acc[k] = s == 0 ? v : acc[k] + v;
     }
     // keep the next input's loads behind this one's stages (register pressure, A/B builds)
@@ -386,14 +399,14 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(
   if constexpr (FUSE) {
 #pragma unroll
     for (int k = 0; k < G::EPT; ++k)
-      col[pidx(brev(own_pos<LC>(tl, k), G::LOG))] = make_double2(acc[k], 0.0);
+      col[pidx<LC>(brev(own_pos<LC>(tl, k), G::LOG))] = make_double2(acc[k], 0.0);
     col_sync<LC>();
     run_stages<LC>(col, tl, tw1f);
     __syncthreads();
     store_rows<LC>(lds, out, item, c0, wbits);
   } else {
 #pragma unroll
-    for (int k = 0; k < G::EPT; ++k) col[pidx(own_pos<LC>(tl, k))] = make_double2(acc[k], 0.0);
+    for (int k = 0; k < G::EPT; ++k) col[pidx<LC>(own_pos<LC>(tl, k))] = make_double2(acc[k], 0.0);
     __syncthreads();
     store_cols<LC>(lds, [&](long it, long i, cplx v) { out(it, i, v.x); }, item, c0, wbits);
   }
@@ -411,7 +424,7 @@ __device__ __forceinline__ void line_load_rev(cplx* col, int tl, const In& in, l
 #pragma unroll
   for (int k = 0; k < G::EPT; ++k) v[k] = in(line, own_pos<LC>(tl, k));
 #pragma unroll
-  for (int k = 0; k < G::EPT; ++k) col[pidx(brev(own_pos<LC>(tl, k), G::LOG))] = v[k];
+  for (int k = 0; k < G::EPT; ++k) col[pidx<LC>(brev(own_pos<LC>(tl, k), G::LOG))] = v[k];
 }
 
 // jw_fft (JW_ARITH_STRICT): In (line, r) -> cplx; Out (line, r, cplx); scale applied to both
@@ -435,7 +448,7 @@ __global__ __launch_bounds__(kNT) void kline_fft(In in, Out out, long nlines,
 #pragma unroll
   for (int k = 0; k < G::EPT; ++k) {
     const int p = own_pos<LC>(tl, k);
-    cplx v = col[pidx(p)];
+    cplx v = col[pidx<LC>(p)];
     if (do_scale) v = jscale(v, scale);
     out(line, p, v);
   }
@@ -472,14 +485,14 @@ __global__ __launch_bounds__(kNT) void kline_modwt(In in, Mid mid, Out out, long
     col_sync<LC>();
     cplx X[G::EPT];
 #pragma unroll
-    for (int k = 0; k < G::EPT; ++k) X[k] = col[pidx(own_pos<LC>(tl, k))];
+    for (int k = 0; k < G::EPT; ++k) X[k] = col[pidx<LC>(own_pos<LC>(tl, k))];
 #pragma unroll
     for (int f = 0; f < NOUT; ++f) {
       col_sync<LC>();
 #pragma unroll
       for (int k = 0; k < G::EPT; ++k) {
         const int p = own_pos<LC>(tl, k);
-        col[pidx(brev(p, G::LOG))] = mid(s, f, p, X[k]);
+        col[pidx<LC>(brev(p, G::LOG))] = mid(s, f, p, X[k]);
       }
       col_sync<LC>();
       run_stages<LC>(col, tl, twi);
@@ -487,7 +500,7 @@ __global__ __launch_bounds__(kNT) void kline_modwt(In in, Mid mid, Out out, long
 #pragma unroll
       for (int k = 0; k < G::EPT; ++k) {
         const int p = own_pos<LC>(tl, k);
-        const double v = col[pidx(p)].x * inv_n;  // result[i].mul(1.0/n).getReal()
+        const double v = col[pidx<LC>(p)].x * inv_n;  // result[i].mul(1.0/n).getReal()
         if constexpr (NOUT == 2) {
           if (valid) out(f, line, p, v);
         } else {
@@ -532,12 +545,12 @@ __global__ __launch_bounds__(kNT) void kline_conv(In in, Out out, long nlines,
   col_sync<LC>();
   cplx X[G::EPT];
 #pragma unroll
-  for (int k = 0; k < G::EPT; ++k) X[k] = col[pidx(own_pos<LC>(tl, k))];
+  for (int k = 0; k < G::EPT; ++k) X[k] = col[pidx<LC>(own_pos<LC>(tl, k))];
   col_sync<LC>();
 #pragma unroll
   for (int k = 0; k < G::EPT; ++k) {
     const int p = own_pos<LC>(tl, k);
-    col[pidx(brev(p, G::LOG))] = jmul(X[k], B[p]);
+    col[pidx<LC>(brev(p, G::LOG))] = jmul(X[k], B[p]);
   }
   col_sync<LC>();
   run_stages<LC>(col, tl, twi);
@@ -546,7 +559,7 @@ __global__ __launch_bounds__(kNT) void kline_conv(In in, Out out, long nlines,
 #pragma unroll
   for (int k = 0; k < G::EPT; ++k) {
     const int p = own_pos<LC>(tl, k);
-    out(line, p, col[pidx(p)]);
+    out(line, p, col[pidx<LC>(p)]);
   }
 }
 
