@@ -33,7 +33,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "modwt_pmc_traffic.json")
 # cwt / fwt2d HBM bytes per step at their default configs (tools/pmc_traffic.sh,
 # tools/traffic_summary.py)
-TRAFFIC_STEP_FILE = os.path.join(ROOT, "profiles", "r04", "final_f", "traffic_cwt_fwt2d.json")
+TRAFFIC_STEP_FILE = os.path.join(ROOT, "profiles", "r04", "final_z", "traffic_cwt_fwt2d.json")
 
 
 def generate_inputs(gen, min_seconds=1.0):
