@@ -52,6 +52,9 @@ __host__ __device__ constexpr int ilog2(long v) {
 #ifndef JF_SWZ  // LDS layout of a column (A/B builds: 0 = one pad slot per 8 points)
 #define JF_SWZ 1
 #endif
+#ifndef JF_SWZ_MIN  // shortest column that takes the swizzle (A/B builds)
+#define JF_SWZ_MIN 1024
+#endif
 template <int LC>
 struct Geo {
   static constexpr int LOG = ilog2(LC);
@@ -62,13 +65,15 @@ struct Geo {
   static constexpr int TPC = LC / EPT;  // threads per column (divides 64 when <= 64)
   static constexpr int T = kNT / TPC;   // columns per workgroup
   // column stride: the XOR-swizzled layout (pidx) needs no padding inside a column, 6 slots
-  // between columns; the padded one (short columns, JF_SWZ=0) one slot per 8 points
-  static constexpr bool SWZ = JF_SWZ && LC >= 128;
+  // between columns; the padded one (columns under 1024 points, JF_SWZ=0) one slot per 8 points.
+  // 512-point columns keep the padding: swizzled, the AUTO inverse's kp2r<512, 2> ran slower
+  // (profiles/r04/ab/auto_swz_min1024_z.log: db4 J=8 1,491 -> 1,519 Msamples/s with the padding)
+  static constexpr bool SWZ = JF_SWZ && LC >= JF_SWZ_MIN;
   static constexpr int CS = SWZ ? LC + 6 : LC + LC / 8 + (LC == 1024 ? 3 : LC == 2048 ? 5 : 1);
   static constexpr size_t LDS_BYTES = (size_t)T * CS * sizeof(cplx);
 };
 
-// LDS slot of column position pos.  Columns of >= 128 points: the low three bits XORed with bits
+// LDS slot of column position pos.  Columns of >= 1024 points: the low three bits XORed with bits
 // 3-5, 6-8 and 9-11 (a permutation inside each group of 8 slots), which spreads the strided
 // and bit-reversed accesses of the stage groups, the staging and the kp2p / kp2r transitions
 // over the banks (a bank model of those phases: 9,984 vs 18,944 conflict-weighted group
