@@ -26,8 +26,14 @@ public class HipContinuousWaveletTransform extends ContinuousWaveletTransform {
   private final int arith;
   private final int device; // -1: the calling thread's current device
 
+  /** The reference's default padding is SYMMETRIC (ContinuousWaveletTransform.java:91-93). */
   public HipContinuousWaveletTransform(ContinuousWavelet w) {
-    this(w, PaddingType.ZERO, HipMODWTTransform.ARITH_STRICT);
+    this(w, PaddingType.SYMMETRIC, HipMODWTTransform.ARITH_STRICT);
+  }
+
+  /** ContinuousWaveletTransform(wavelet, paddingType) (:101-106), STRICT arithmetic. */
+  public HipContinuousWaveletTransform(ContinuousWavelet w, PaddingType p) {
+    this(w, p, HipMODWTTransform.ARITH_STRICT);
   }
 
   public HipContinuousWaveletTransform(ContinuousWavelet w, PaddingType p, int arith) {

@@ -45,13 +45,19 @@ public class HipMODWTTransform extends MODWTTransform {
     }
   }
 
-  public HipMODWTTransform(Wavelet w) { this(w, ARITH_STRICT); }
-
-  public HipMODWTTransform(Wavelet w, int arith) {
+  /** MODWTTransform(wavelet) (:180-183): threshold 4096 (:144), AUTO (:167), STRICT. */
+  public HipMODWTTransform(Wavelet w) {
     super(w);
-    this.arith = arith;
+    this.arith = ARITH_STRICT;
     this.device = -1;
   }
+
+  /**
+   * MODWTTransform(wavelet, fftThreshold) (:191-194), STRICT.  The second int is the threshold,
+   * as in the reference, so {@code new HipMODWTTransform(w, 8192)} means what it means there;
+   * the arithmetic contract takes the three-argument form.
+   */
+  public HipMODWTTransform(Wavelet w, int fftThreshold) { this(w, fftThreshold, ARITH_STRICT, -1); }
 
   public HipMODWTTransform(Wavelet w, int fftThreshold, int arith) { this(w, fftThreshold, arith, -1); }
 

@@ -576,8 +576,9 @@ static bool auto_level_fft(long n, int L, int j, int threshold) {
 //   JW_ARITH_STRICT (the JVM's arithmetic): every level takes the convolution the reference's
 //     performConvolution takes (:640-664) -- FFT always, DIRECT never, AUTO by the int32
 //     N*M_j > fftConvolutionThreshold rule -- and FFT levels run the reference's own FFT
-//     (jw_jfft.hip), so results are the JVM's bit for bit.  Lengths that path does not take yet
-//     run the exact-twiddle pyramid (jw_modwt_fft.hip) when any level is FFT.
+//     (jw_jfft.hip), so results are the JVM's bit for bit.  A length outside that path's range
+//     (kStrictFftPow2Max / kStrictFftOtherMax, jw_internal.hpp) is JW_ERR_UNSUPPORTED when any
+//     level is FFT: the exact-twiddle pyramid is never a STRICT result.
 //   JW_ARITH_FMA (fast contract): FFT runs the exact-twiddle frequency-domain pyramid; AUTO and
 //     DIRECT run the direct kernels, which are faster and more accurate than any FFT path here.
 //   A level the reference would run through its FFT at a length the FFT paths do not take
@@ -598,8 +599,7 @@ static ModwtPath modwt_path(const ModwtPlan& p, int method, long n, int levels, 
     return modwt_fft_supported(n) ? ModwtPath::kPyramid : ModwtPath::kUnsupported;
   }
   if (!any) return ModwtPath::kDirect;
-  if (modwt_strict_fft_supported(n)) return ModwtPath::kStrictLevels;
-  return modwt_fft_supported(n) ? ModwtPath::kPyramid : ModwtPath::kUnsupported;
+  return modwt_strict_fft_supported(n) ? ModwtPath::kStrictLevels : ModwtPath::kUnsupported;
 }
 
 static int modwt_unsupported(int arith, int method, long n, const bool* fft, int levels) {

@@ -196,6 +196,16 @@ int modwt_forward_device(const ModwtPlan& p, const double* x, double* coeffs, lo
                          int batch, hipStream_t s);
 int modwt_inverse_device(const ModwtPlan& p, const double* coeffs, double* x, long n, int J,
                          int batch, hipStream_t s);
+// FFT-path length ranges (inclusive, n >= 2).  The FMA pyramid (jw_modwt_fft.hip) takes
+// n <= kPyramidFftMax; STRICT (JWave's own FFT, jw_jfft.hip) takes powers of two up to
+// kStrictFftPow2Max and other n up to kStrictFftOtherMax (Bluestein, m <= 2^28).  A STRICT level
+// outside its range is JW_ERR_UNSUPPORTED, never the pyramid (not JWave's arithmetic): that is
+// only sound while the STRICT range covers the pyramid's, which the assertion pins.
+constexpr long kPyramidFftMax = 1L << 23;
+constexpr long kStrictFftPow2Max = 1L << 28;
+constexpr long kStrictFftOtherMax = kStrictFftPow2Max / 2;
+static_assert(kPyramidFftMax <= kStrictFftOtherMax && kStrictFftOtherMax <= kStrictFftPow2Max,
+              "the STRICT FFT range must contain the FMA pyramid's");
 bool modwt_fft_supported(long n);
 int modwt_forward_fft_device(const ModwtPlan& p, const double* x, double* coeffs, long n, int J,
                              int batch, hipStream_t s);

@@ -575,7 +575,7 @@ int modwt_strict(bool inverse, const ModwtPlan& p, const double* in, double* out
 // every length the reference's FFT path takes here: powers of two (radix 2) up to 2^28 and,
 // through Bluestein with m <= 2^28, any other n <= 2^27
 bool modwt_strict_fft_supported(long n) {
-  return n >= 2 && n <= ((n & (n - 1)) == 0 ? jf::kStrictPow2Max : jf::kStrictPow2Max / 2);
+  return n >= 2 && n <= ((n & (n - 1)) == 0 ? kStrictFftPow2Max : kStrictFftOtherMax);
 }
 
 int modwt_forward_strict_device(const ModwtPlan& p, const double* x, double* coeffs, long n,
@@ -597,7 +597,7 @@ int fft_strict_device(int S, const double* in, double* out, long n, long batch, 
     return JW_OK;
   }
   if ((n & (n - 1)) != 0) {
-    if (n > jf::kStrictPow2Max / 2)
+    if (n > kStrictFftOtherMax)
       return fail(JW_ERR_UNSUPPORTED, "Java-order FFT: length %ld > 2^27", n);
     return jf::bs_fft_strict(S > 0, (const jf::cplx*)in, (jf::cplx*)out, n, batch, s);
   }

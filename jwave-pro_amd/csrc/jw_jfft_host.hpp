@@ -28,7 +28,7 @@ inline int split_lc1(long n) { return n <= kLineMax ? (int)n : 1 << (ilog2(n) / 
 // default; env JW_JFFT_3PASS_MIN (a power of two >= 2^18) lowers it, so the tests can check the
 // three-pass code against the oracle at sizes the oracle finishes quickly.
 long three_pass_min();
-constexpr long kStrictPow2Max = 1L << 28;  // the longest power-of-two STRICT transform
+constexpr long kStrictPow2Max = kStrictFftPow2Max;  // the longest power-of-two STRICT transform
 // bits of A, B, C for a three-pass n = 2^lg (18 <= lg <= 36)
 inline void split3(int lg, int* a, int* b, int* c) {
   *a = std::min(12, lg - 12);

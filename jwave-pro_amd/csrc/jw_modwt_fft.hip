@@ -468,7 +468,7 @@ int fft_device(int S, const double* in, double* out, long n, long batch, hipStre
 static bool is_pow2(long N) { return (N & (N - 1)) == 0; }
 
 // power-of-two N: the four-step pyramid; other N (< 2^23): the chirp-z pyramid
-bool modwt_fft_supported(long N) { return N >= 2 && N <= (1L << 23); }
+bool modwt_fft_supported(long N) { return N >= 2 && N <= kPyramidFftMax; }
 
 namespace {
 // ---------------------------------------------------------------------------------------

@@ -395,3 +395,31 @@ def test_strict_fft_past_its_range_is_unsupported():
                                    _native.JW_ARITH_STRICT, _native.JW_HOST, None)
         msg = _native.last_error()
         assert st == _native.JW_ERR_UNSUPPORTED and "2^28" in msg and "2^27" in msg, msg
+
+
+def test_strict_range_contains_the_pyramid_range():
+    # verdict r04 item 6: a STRICT level outside JWave's FFT range is JW_ERR_UNSUPPORTED, never
+    # the FMA pyramid; that is sound only while the STRICT range contains the pyramid's
+    # (static_assert in jw_internal.hpp).  Read both limits back from the C-ABI's own messages.
+    lib = _native.lib()
+    vp = ctypes.c_void_p
+    wv = W.Daubechies4()
+    sd, wd = np.asarray(wv.getScalingDeComposition()), np.asarray(wv.getWaveletDeComposition())
+    n = 1 << 29
+    x = np.zeros(1)
+    msgs = {}
+    for arith in (_native.JW_ARITH_STRICT, _native.JW_ARITH_FMA):
+        plan = vp()
+        assert lib.jw_modwt_plan_create(ctypes.byref(plan), vp(sd.ctypes.data), vp(wd.ctypes.data),
+                                        8, 4096, arith) == _native.JW_OK
+        # the range check precedes every read of the buffers (JW_DEVICE: nothing is staged)
+        st = lib.jw_modwt_forward(plan, vp(x.ctypes.data), vp(x.ctypes.data), n, 1, 1,
+                                  _native.JW_CONV_FFT, _native.JW_DEVICE, None)
+        assert st == _native.JW_ERR_UNSUPPORTED
+        msgs[arith] = _native.last_error()
+        lib.jw_modwt_plan_destroy(plan)
+    lim = {a: [int(v) for v in re.findall(r"\((\d+)\)", m)] for a, m in msgs.items()}
+    pow2_max, other_max = lim[_native.JW_ARITH_STRICT]
+    (pyr_max,) = lim[_native.JW_ARITH_FMA]
+    assert (pow2_max, other_max, pyr_max) == (1 << 28, 1 << 27, 1 << 23)
+    assert pyr_max <= other_max <= pow2_max

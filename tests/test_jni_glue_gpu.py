@@ -131,6 +131,27 @@ def test_cwt_fft_scalogram_and_direct(jni):
     assert bits_equal(rows[:, 0::2], refd.real) and bits_equal(rows[:, 1::2], refd.imag)
 
 
+@pytest.mark.parametrize("padding", [0, 1, 2, 3], ids=["zero", "symmetric", "periodic", "constant"])
+@pytest.mark.parametrize("n", [3000, 70001])
+def test_cwt_fft_every_padding_non_power_of_two(jni, n, padding):
+    # ContinuousWaveletTransform.java:183-229 with each PaddingType (the ordinal the Java
+    # drop-in passes, :29-44; SYMMETRIC = 1 is the one-argument constructor's default, :91-93):
+    # n = 3000 pads to 4096, n = 70001 to 131072, so the extension is most of the line
+    fb, fc = 1.0, 6.0 / (2 * np.pi)
+    x = orc.fill_uniform(n, 100 + n + padding)
+    scales = np.exp(np.log(2.0) + np.arange(10) * (np.log(1024.0) - np.log(2.0)) / 9)
+    prm = jni.darray(np.array([fb, fc]))
+    rows = jni.read(jni.call("HipContinuousWaveletTransform_nTransformFFT", 0, prm, jni.darray(x),
+                             jni.darray(scales), 1.0, padding))
+    assert rows.shape == (len(scales), 2 * n)
+    got = rows[:, 0::2] + 1j * rows[:, 1::2]
+    ref = orc.cwt_fft(x, scales, 1.0, "morlet", (fb, fc), padding, exact=True)
+    assert np.max(np.abs(got - ref)) / np.max(np.abs(ref)) < 1e-12
+    # and against JWave's own recurrence-twiddle FFT path, north_star's 1e-10 relative
+    jref = orc.cwt_fft(x, scales, 1.0, "morlet", (fb, fc), padding, exact=False)
+    assert np.max(np.abs(got - jref)) / np.max(np.abs(jref)) < 1e-10
+
+
 @pytest.mark.parametrize("n", [1024, 1 << 14, 1000])
 def test_fft_strict_matches_reference_fft(jni, n):
     rng = np.random.default_rng(n)

@@ -280,6 +280,39 @@ def test_full_size_properties(device):
     assert bits_equal(c[1].cpu().numpy(), ref)
 
 
+def test_cfg2_headline_fma_full_size(device):
+    # The headline's own arithmetic at the headline size (BASELINE configs[1]: db4, J = 8,
+    # N = 2^20, JW_ARITH_FMA, DIRECT -- what bench.py times): two jw_synth_uniform signals,
+    # every coefficient row within 1e-10 normwise of the oracle's DIRECT path
+    # (MODWTTransform.java:256-306), the inverse of the oracle's coefficients within 1e-10 of
+    # the oracle's inverse (:337-375), and the round trip as exact as JWave's own.
+    import ctypes
+    import torch
+    from jwave import _native
+    wv = W.Daubechies4()
+    g, h = ofilters(wv)
+    B, n, J = 2, 1 << 20, 8
+    x = torch.empty((B, n), dtype=torch.float64, device=device)
+    _native.check(_native.lib().jw_synth_uniform(ctypes.c_void_p(x.data_ptr()), n, B, 42, None))
+    m = direct(wv, arith="fma")
+    c = m.forwardMODWT(x, J)
+    xr = m.inverseMODWT(c)
+    torch.cuda.synchronize()
+    for b in range(B):
+        xb = orc.fill_uniform(n, 42 + b)
+        ref = orc.modwt_forward(xb, J, g, h, "direct_nz")
+        got = c[b].cpu().numpy()
+        for r in range(J + 1):
+            assert normwise(got[r], ref[r]) < FMA_TOL, (b, r)
+        rec = orc.modwt_inverse(ref, g, h, "direct_nz")
+        assert normwise(m.inverseMODWT(ref), rec) < FMA_TOL
+        ref_err = np.max(np.abs(rec - xb))
+        assert np.max(np.abs(xr[b].cpu().numpy() - xb)) <= 2 * ref_err + 1e-13
+    # north_star's "perfect reconstruction < 1e-12" holds as RMS; max-abs is JWave's class
+    rms = torch.sqrt(torch.mean((xr - x) ** 2)).item()
+    assert rms < 1e-12, rms
+
+
 @pytest.mark.parametrize("arith", ["strict", "fma"])
 def test_cfg5_geometry_full_size(arith, device):
     # BASELINE configs[4] kernel: Symlet8, J = 6, N = 2^20 -- two signals against the oracle
@@ -306,6 +339,7 @@ def test_cfg5_geometry_full_size(arith, device):
         else:
             for r in range(J + 1):
                 assert normwise(got[r], ref[r]) < FMA_TOL
+            assert normwise(m.inverseMODWT(ref), rec) < FMA_TOL
     assert (xr - x).abs().max().item() < 1e-11
 
 
