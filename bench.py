@@ -288,7 +288,7 @@ def main_cwt(args, dev, rank, world):
                          "algorithmic_bytes_per_launch": per_call,
                          "note": "one launch = one jw_cwt_fft call over the batch (all FFT "
                                  "passes); traffic = rocprofv3 FETCH_SIZE*2 + WRITE_SIZE per call "
-                                 "(profiles/r04/final_f/traffic_cwt_fwt2d.json): the A workspace round "
+                                 f"({os.path.relpath(TRAFFIC_STEP_FILE, ROOT)}): the A workspace round "
                                  "trip of the two-pass scales is the excess over algorithmic; the "
                                  "band scales (cwt_band512) run in one pass.  The structure's own "
                                  "floor (34 two-pass scales at 3x their output, 30 one-pass) is "

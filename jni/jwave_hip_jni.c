@@ -350,45 +350,102 @@ JNIEXPORT jobjectArray JNICALL Java_jwave_hip_HipFastWaveletTransform_nMatrix(
   return out;
 }
 
+/* The exceptions the reference's own array indexing throws (the JVM's messages). */
+static void npe(JNIEnv* env) {
+  jclass c = (*env)->FindClass(env, "java/lang/NullPointerException");
+  if (c) (*env)->ThrowNew(env, c, NULL);
+}
+static void aioobe(JNIEnv* env, jsize index, jsize length) {
+  char msg[96];
+  snprintf(msg, sizeof msg, "Index %d out of bounds for length %d", (int)index, (int)length);
+  jclass c = (*env)->FindClass(env, "java/lang/ArrayIndexOutOfBoundsException");
+  if (c) (*env)->ThrowNew(env, c, msg);
+}
+
+/* Box [0, d2) x [0, d3) of one slab into dst, read the way BasicTransform.java:518-528 reads
+ * spcTime[i][j][k]: a null slab or row throws NullPointerException, one shorter than the box
+ * ArrayIndexOutOfBoundsException, and anything past the box is ignored.  0 = exception pending. */
+static int slab_in(JNIEnv* env, jobjectArray m, jsize d2, jsize d3, double* dst) {
+  if (!m) {
+    npe(env);
+    return 0;
+  }
+  const jsize r = (*env)->GetArrayLength(env, m);
+  for (jsize j = 0; j < d2 && d3 > 0; ++j) {
+    if (j >= r) {
+      aioobe(env, j, r);
+      return 0;
+    }
+    jdoubleArray row = (jdoubleArray)(*env)->GetObjectArrayElement(env, m, j);
+    if ((*env)->ExceptionCheck(env)) return 0;
+    if (!row) {
+      npe(env);
+      return 0;
+    }
+    const jsize c = (*env)->GetArrayLength(env, row);
+    if (c < d3) aioobe(env, c, c);
+    else (*env)->GetDoubleArrayRegion(env, row, 0, d3, dst + (size_t)j * d3);
+    (*env)->DeleteLocalRef(env, row);
+    if (c < d3) return 0;
+  }
+  return 1;
+}
+
 /* 3-D: op 0 forward, 1 reverse (double[][][] spc, lvlP, lvlQ, lvlR), BasicTransform.java:509/:602.
- * Every [d2][d3] slab must have the shape of the first one. */
+ * The shape is slab 0's (noOfRows = spc.length, noOfCols = spc[0].length, noOfHigh =
+ * spc[0][0].length, :512-514 / :605-607), every slab is read over that box (slab_in). */
 JNIEXPORT jobjectArray JNICALL Java_jwave_hip_HipFastWaveletTransform_nSpace(
     JNIEnv* env, jclass cls, jlong plan, jint op, jobjectArray in, jint lvlP, jint lvlQ,
     jint lvlR) {
   (void)cls;
-  const jsize d1 = in ? (*env)->GetArrayLength(env, in) : 0;
-  jsize d2 = 0, d3 = 0;
-  double* x = NULL;
-  size_t slab = 0;
+  if (!in) {  // spcTime.length
+    npe(env);
+    return NULL;
+  }
+  const jsize d1 = (*env)->GetArrayLength(env, in);
+  if (d1 == 0) {  // spcTime[0]
+    aioobe(env, 0, 0);
+    return NULL;
+  }
+  jobjectArray m0 = (jobjectArray)(*env)->GetObjectArrayElement(env, in, 0);
+  if ((*env)->ExceptionCheck(env)) return NULL;
+  if (!m0) {  // spcTime[0].length
+    npe(env);
+    return NULL;
+  }
+  const jsize d2 = (*env)->GetArrayLength(env, m0);
+  if (d2 == 0) {  // spcTime[0][0]
+    (*env)->DeleteLocalRef(env, m0);
+    aioobe(env, 0, 0);
+    return NULL;
+  }
+  jdoubleArray r00 = (jdoubleArray)(*env)->GetObjectArrayElement(env, m0, 0);
+  (*env)->DeleteLocalRef(env, m0);
+  if ((*env)->ExceptionCheck(env)) return NULL;
+  if (!r00) {  // spcTime[0][0].length
+    npe(env);
+    return NULL;
+  }
+  const jsize d3 = (*env)->GetArrayLength(env, r00);
+  (*env)->DeleteLocalRef(env, r00);
+  const size_t slab = (size_t)d2 * d3;
+  double* x = malloc(sizeof(double) * (size_t)d1 * (slab ? slab : 1));
+  if (!x) {
+    oom(env);
+    return NULL;
+  }
   for (jsize i = 0; i < d1; ++i) {
     jobjectArray m = (jobjectArray)(*env)->GetObjectArrayElement(env, in, i);
     if ((*env)->ExceptionCheck(env)) {
       free(x);
       return NULL;
     }
-    jsize r = 0, c = 0;
-    double* part = m ? rows_in(env, m, &r, &c) : NULL;
+    const int ok = slab_in(env, m, d2, d3, x + (size_t)i * slab);
     if (m) (*env)->DeleteLocalRef(env, m);
-    if (!part) {
+    if (!ok) {
       free(x);
-      if (!(*env)->ExceptionCheck(env)) iae(env, "Space slabs must all have the same shape");
       return NULL;
     }
-    if (i == 0) {
-      d2 = r, d3 = c, slab = (size_t)d2 * d3;
-      x = malloc(sizeof(double) * (size_t)d1 * (slab ? slab : 1));
-      if (!x) {
-        free(part);
-        oom(env);
-        return NULL;
-      }
-    } else if (r != d2 || c != d3) {
-      free(part), free(x);
-      iae(env, "Space slabs must all have the same shape");
-      return NULL;
-    }
-    for (size_t k = 0; k < slab; ++k) x[(size_t)i * slab + k] = part[k];
-    free(part);
   }
   double* y = malloc(sizeof(double) * (size_t)d1 * (slab ? slab : 1));
   if (!y) {

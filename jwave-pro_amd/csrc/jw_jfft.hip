@@ -86,7 +86,10 @@ long three_pass_min() {
 }
 
 using Tw3Key = std::tuple<int, long, int>;  // device, n, inverse (the split is a function of n)
-DevCache<Tw3Key> g_tw3(kCacheBytes);
+// The three-pass tables are (A + AB + n) x 16 bytes: 1.08 GB at 2^26, 4.3 GB at 2^28 per
+// direction.  Their own budget holds both directions at 2^28, so the longest transforms keep
+// their tables instead of rebuilding multi-GB host tables on every call.
+DevCache<Tw3Key> g_tw3(10UL << 30);
 
 int twiddles3(long n, bool inverse, Tw3* out, StreamAllocs& mem, hipStream_t s) {
   int dev = 0;
@@ -452,8 +455,16 @@ int modwt_strict_long(bool inverse, const ModwtPlan& p, const double* in, double
   JW_HIP_TRY(mem.alloc(&tmp, (size_t)2 * N * sizeof(double)));
   const double inv_n = 1.0 / (double)N;
   int st = JW_OK;
+  // Each transform takes its workspace (and, past the table cache's budget, its three-pass
+  // twiddles) from an allocator scoped to that one call, freed stream-ordered when it returns:
+  // with the call's own allocator they would pile up over batch x levels x transforms until
+  // modwt_strict returns (~7.5 GB per signal at 2^25, db4 J=8).
+  auto rows = [&](bool inv, auto in, auto out) {
+    StreamAllocs scoped(s);
+    return fft_rows(N, inv, 1, in, out, scoped, s);
+  };
   auto fwd = [&](const double* v) {  // X = FFT(Complex(v, 0))
-    return fft_rows(N, false, 1, RowsR{v, N}, OutCS{X, N, 1.0, 0}, mem, s);
+    return rows(false, RowsR{v, N}, OutCS{X, N, 1.0, 0});
   };
   for (long b = 0; b < batch && st == JW_OK; ++b) {
     if (!inverse) {
@@ -467,10 +478,9 @@ int modwt_strict_long(bool inverse, const ModwtPlan& p, const double* in, double
           st = modwt_level_forward_device(p, j, vin, N, w, rs, vout, N, N, 1, s);
         } else if ((st = fwd(vin)) == JW_OK &&
                    (st = mul_spec<false>(X, spec_h(F, N, j), P, N, s)) == JW_OK &&
-                   (st = fft_rows(N, true, 1, RowsC{P, N}, OutRe<false>{w, N, inv_n}, mem, s)) ==
-                       JW_OK &&
+                   (st = rows(true, RowsC{P, N}, OutRe<false>{w, N, inv_n})) == JW_OK &&
                    (st = mul_spec<false>(X, spec_g(F, N, j), P, N, s)) == JW_OK) {
-          st = fft_rows(N, true, 1, RowsC{P, N}, OutRe<false>{vout, N, inv_n}, mem, s);
+          st = rows(true, RowsC{P, N}, OutRe<false>{vout, N, inv_n});
         }
         vin = vout;
       }
@@ -485,12 +495,11 @@ int modwt_strict_long(bool inverse, const ModwtPlan& p, const double* in, double
           st = modwt_level_inverse_device(p, j, vin, N, w, rs, vout, N, N, 1, s);
         } else if ((st = fwd(vin)) == JW_OK &&
                    (st = mul_spec<true>(X, spec_g(F, N, j), P, N, s)) == JW_OK &&
-                   (st = fft_rows(N, true, 1, RowsC{P, N}, OutRe<false>{vout, N, inv_n}, mem,
-                                  s)) == JW_OK &&
+                   (st = rows(true, RowsC{P, N}, OutRe<false>{vout, N, inv_n})) == JW_OK &&
                    (st = fwd(w)) == JW_OK &&
                    (st = mul_spec<true>(X, spec_h(F, N, j), P, N, s)) == JW_OK) {
           // vFromApprox[i] + vFromDetail[i] (:366-369)
-          st = fft_rows(N, true, 1, RowsC{P, N}, OutRe<true>{vout, N, inv_n}, mem, s);
+          st = rows(true, RowsC{P, N}, OutRe<true>{vout, N, inv_n});
         }
         vin = vout;
       }

@@ -48,6 +48,21 @@ __device__ __forceinline__ rsrc_t make_rsrc(const double* p, long n) {
 __device__ __forceinline__ double bload(rsrc_t r, int off) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
 }
+// Cache-policy bits of the streamed HBM accesses of the fused MODWT kernels (A/B builds only:
+// gfx950 aux bits sc0 = 1, nt = 2, sc1 = 16; 0 = the default policy, the product's choice).
+#ifndef JW_FWD_SCP
+#define JW_FWD_SCP 0  // forward: coefficient stores
+#endif
+#ifndef JW_FWD_LCP
+#define JW_FWD_LCP 0  // forward: signal loads
+#endif
+#ifndef JW_INV_LCP
+#define JW_INV_LCP 0  // inverse: coefficient loads
+#endif
+template <int CP>
+__device__ __forceinline__ double bload_cp(rsrc_t r, int off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, CP));
+}
 // non-temporal (streamed once): gives the line up early so rows that are re-read stay in L2
 __device__ __forceinline__ double bload_nt(rsrc_t r, int off) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 2));
@@ -108,8 +123,9 @@ struct GeoF {
   static constexpr int total = H + J * C + 2;  // doubles
 };
 
+template <int CP = 0>
 __device__ __forceinline__ d2 bload2(rsrc_t r, int off) {
-  return __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  return __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, CP));
 }
 template <int CP = 0>
 __device__ __forceinline__ void bstore2(rsrc_t r, int off, d2 v) {
@@ -226,7 +242,7 @@ __global__ __launch_bounds__(NT) void modwt_fwd_fast(const double* __restrict__ 
   auto fetch = [&](d2& dst) {
     int p = lb + 2 * t;
     p = p >= Ni ? p - Ni : p;
-    dst = bload2(rx, p * 8);
+    dst = bload2<JW_FWD_LCP>(rx, p * 8);
     lb += C;
     if (lb >= Ni) lb -= Ni;
   };
@@ -575,9 +591,9 @@ int launch_fwd(const Taps& t, const double* x, double* c, long N, int batch, hip
   const long cs = (long)(J + 1) * N;
   const char* g1 = std::getenv("JW_FWD_ONE_RSRC");  // A/B runs: 0 = one resource per row
   if (cs * 8 < (long)kOOB && !(g1 && g1[0] == '0'))
-    return launch(modwt_fwd_fast<L, J, FMA, NT, 0, true>, lds, nseg, batch, NT, s, x, N, c, cs, N,
+    return launch(modwt_fwd_fast<L, J, FMA, NT, JW_FWD_SCP, true>, lds, nseg, batch, NT, s, x, N, c, cs, N,
                   seg, warm, npairs, t);
-  return launch(modwt_fwd_fast<L, J, FMA, NT>, lds, nseg, batch, NT, s, x, N, c, cs, N, seg, warm,
+  return launch(modwt_fwd_fast<L, J, FMA, NT, JW_FWD_SCP>, lds, nseg, batch, NT, s, x, N, c, cs, N, seg, warm,
                 npairs, t);
 }
 

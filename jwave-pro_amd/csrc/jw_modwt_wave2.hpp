@@ -234,7 +234,7 @@ __global__ __launch_bounds__(64) void modwt_inv_wave2(const double* __restrict__
     auto ld = [&](int row, int k) -> double {
       int p = lb + k;
       p = p >= Ni ? p - Ni : p;
-      return MEM ? bload(rrs(row), roff(row, p)) : (double)(p + row);
+      return MEM ? fast::bload_cp<JW_INV_LCP>(rrs(row), roff(row, p)) : (double)(p + row);
     };
     [&]<int... js>(std::integer_sequence<int, js...>) {
       (([&] {

@@ -132,14 +132,50 @@ def test_fwt_failures_map_to_jwavefailure(jni):
     jni.call("HipFastWaveletTransform_nPlanDestroy", p)
 
 
-def test_fwt_space_ragged_is_iae(jni):
+NPE = "java/lang/NullPointerException"
+AIOOBE = "java/lang/ArrayIndexOutOfBoundsException"
+
+
+def test_fwt_space_malformed_throws_what_the_reference_throws(jni):
+    # BasicTransform.forward/reverse(double[][][], ...) (:509-528, :602-621) take the shape from
+    # spc.length, spc[0].length, spc[0][0].length and copy spc[i][j][k] over that box: a null
+    # array or slab throws NullPointerException, an empty one or a slab shorter than slab 0
+    # ArrayIndexOutOfBoundsException (the glue threw IllegalArgumentException, or
+    # went on with zero dimensions)
+    import ctypes
     p = _fwt_plan(jni, W.Haar1())
-    o = jni.L.mock_oarray(2, b"[[D")
-    jni.L.mock_oset(o, 0, jni.matrix(np.ones((4, 8))))
-    jni.L.mock_oset(o, 1, jni.matrix(np.ones((4, 4))))
-    with pytest.raises(JavaException) as e:
-        jni.call("HipFastWaveletTransform_nSpace", p, 0, o, 1, 1, 1)
-    assert e.value.cls == IAE and "same shape" in e.value.msg
+    for op in (0, 1):
+        with pytest.raises(JavaException) as e:
+            jni.call("HipFastWaveletTransform_nSpace", p, op, ctypes.c_void_p(None), 1, 1, 1)
+        assert e.value.cls == NPE
+        with pytest.raises(JavaException) as e:
+            jni.call("HipFastWaveletTransform_nSpace", p, op, jni.L.mock_oarray(0, b"[[D"), 1, 1, 1)
+        assert e.value.cls == AIOOBE and "Index 0 out of bounds for length 0" in e.value.msg
+        with pytest.raises(JavaException) as e:  # spc[0] == null
+            jni.call("HipFastWaveletTransform_nSpace", p, op, jni.L.mock_oarray(2, b"[[D"), 1, 1, 1)
+        assert e.value.cls == NPE
+        with pytest.raises(JavaException) as e:  # spc[0].length == 0: spc[0][0]
+            o = jni.L.mock_oarray(2, b"[[D")
+            jni.L.mock_oset(o, 0, jni.L.mock_oarray(0, b"[D"))
+            jni.call("HipFastWaveletTransform_nSpace", p, op, o, 1, 1, 1)
+        assert e.value.cls == AIOOBE
+        with pytest.raises(JavaException) as e:  # slab 1 narrower than slab 0
+            o = jni.L.mock_oarray(2, b"[[D")
+            jni.L.mock_oset(o, 0, jni.matrix(np.ones((4, 8))))
+            jni.L.mock_oset(o, 1, jni.matrix(np.ones((4, 4))))
+            jni.call("HipFastWaveletTransform_nSpace", p, op, o, 1, 1, 1)
+        assert e.value.cls == AIOOBE and "Index 4 out of bounds for length 4" in e.value.msg
+        with pytest.raises(JavaException) as e:  # slab 1 with fewer rows
+            o = jni.L.mock_oarray(2, b"[[D")
+            jni.L.mock_oset(o, 0, jni.matrix(np.ones((4, 8))))
+            jni.L.mock_oset(o, 1, jni.matrix(np.ones((2, 8))))
+            jni.call("HipFastWaveletTransform_nSpace", p, op, o, 1, 1, 1)
+        assert e.value.cls == AIOOBE and "Index 2 out of bounds for length 2" in e.value.msg
+        with pytest.raises(JavaException) as e:  # a null slab past the first
+            o = jni.L.mock_oarray(2, b"[[D")
+            jni.L.mock_oset(o, 0, jni.matrix(np.ones((4, 8))))
+            jni.call("HipFastWaveletTransform_nSpace", p, op, o, 1, 1, 1)
+        assert e.value.cls == NPE
     jni.call("HipFastWaveletTransform_nPlanDestroy", p)
 
 

@@ -106,6 +106,16 @@ def test_fwt_matrix_and_space_bit_exact(jni, wname):
     assert ys.shape == s.shape and bits_equal(ys, orc.fwt3d_forward(s, 4, 5, 3, wv))
     zs = jni.read(jni.call("HipFastWaveletTransform_nSpace", p, 1, jni.space(ys), 4, 5, 3))
     assert bits_equal(zs, orc.fwt3d_reverse(ys, 4, 5, 3, wv))
+    # slabs past the first may be larger: the reference copies slab 0's box of each and ignores
+    # the rest (BasicTransform.java:518-528)
+    o = jni.L.mock_oarray(s.shape[0], b"[[D")
+    for i in range(s.shape[0]):
+        big = rng.uniform(-1, 1, (16 + i % 3, 32 + 2 * (i % 2))) if i else s[0]
+        if i:
+            big[:16, :32] = s[i]
+        jni.L.mock_oset(o, i, jni.matrix(big))
+    yb = jni.read(jni.call("HipFastWaveletTransform_nSpace", p, 0, o, 4, 5, 3))
+    assert yb.shape == s.shape and bits_equal(yb, ys)
     jni.call("HipFastWaveletTransform_nPlanDestroy", p)
 
 

@@ -254,6 +254,43 @@ def test_modwt_long_lines_bit_exact(wname, n, J, threshold, method, monkeypatch)
         assert bits_equal(xr[b], orc.modwt_inverse(ref, g, h, method, threshold)), b
 
 
+def test_long_lines_workspace_bounded(monkeypatch, device):
+    # modwt_strict_long handed its own allocator to every transform, so the
+    # three-pass workspaces piled up over batch x levels x transforms (db4 J=8, 8 signals at
+    # 2^18: 8 x 56 transforms x 4 MB = 1.8 GB).  Each transform's workspace is now scoped to it:
+    # the device memory a batch-8 call reserves stays bounded by a few line-sized buffers.
+    import ctypes
+    import torch
+    from jwave import _native
+    monkeypatch.setenv("JW_JFFT_3PASS_MIN", str(1 << 18))
+    n, J, B = 1 << 18, 8, 8
+    wv = W.Daubechies4()
+    x = torch.empty((B, n), dtype=torch.float64, device=device)
+    _native.check(_native.lib().jw_synth_uniform(ctypes.c_void_p(x.data_ptr()), n, B, 3, None))
+    c = torch.empty((B, J + 1, n), dtype=torch.float64, device=device)
+    xr = torch.empty_like(x)
+    m = MODWTTransform(wv)  # AUTO STRICT: every level through the long-line path at 2^18
+    plan = m.initializeFilterCache()
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+
+    def run(b):
+        _native.check(_native.lib().jw_modwt_forward(plan, P(x), P(c), n, J, b, _native.JW_CONV_AUTO,
+                                                     _native.JW_DEVICE, None))
+        _native.check(_native.lib().jw_modwt_inverse(plan, P(c), P(xr), n, J, b, _native.JW_CONV_AUTO,
+                                                     _native.JW_DEVICE, None))
+        torch.cuda.synchronize()
+
+    run(1)  # tables (twiddles, filter spectra) and one signal's workspaces
+    free0 = torch.cuda.mem_get_info(device)[0]
+    run(B)
+    grew = free0 - torch.cuda.mem_get_info(device)[0]
+    assert grew < (256 << 20), f"batch {B} reserved {grew / 2**20:.0f} MiB more than batch 1"
+    g, h = ofilters(wv)
+    ref = orc.modwt_forward(orc.fill_uniform(n, 3 + B - 1), J, g, h, "auto")
+    assert bits_equal(c[B - 1].cpu().numpy(), ref)
+    assert bits_equal(xr[B - 1].cpu().numpy(), orc.modwt_inverse(ref, g, h, "auto"))
+
+
 @pytest.mark.parametrize("lg", [25, 26, 27])
 def test_fft_strict_three_pass_default_geometry(lg):
     # past the two-pass split, with the default geometry (jw_jfft_host.hpp split3: 2^12 x 2^6 x
