@@ -11,6 +11,8 @@
 #             traffic FETCH_SIZE and WRITE_SIZE passes (separate runs, kernel trace only)
 #             sq      SQ activity / VALU / MFMA-busy / LDS counters (one pass, kernel trace only)
 #             ab      same-box A/B of library builds (LIBS="base v1 ..", REPS rounds)
+#             envab   same-box A/B of environment settings (ENVS="base;K=V;K=V K2=V2", REPS
+#                     rounds; STATS=1 adds a kernel trace per setting)
 #             final   tests, smoke, bench_all, then stats + traffic of modwt and cwt
 #   WORKLOAD  modwt (headline, default) | sym8 (cfg5) | cwt (cfg3) | fwt2d (cfg4) |
 #             auto (JWave's default path: AUTO STRICT db4 J=8, 128 x 2^20, tools/modwt_time.py)
@@ -119,6 +121,31 @@ keys = [k for k in list(d) + list(r) if k.endswith('_ms') or k in ('value', 'msa
 print('$L', {k: d.get(k, r.get(k)) for k in keys})" | tee -a "$O/ab_${w}.txt"
         done
       done ;;
+    envab)
+      # same-box A/B of environment settings, alternating: ENVS="base;JW_X=1;JW_X=1 JW_Y=0"
+      # (base = no extra settings), REPS rounds; with STATS=1 also a kernel-trace per setting
+      IFS=';' read -r -a sets <<< "${ENVS:?ENVS}"
+      for rep in $(seq "${REPS:-2}"); do
+        for i in "${!sets[@]}"; do
+          e="${sets[$i]}"; [ "$e" = base ] && e=""
+          # shellcheck disable=SC2046,SC2086
+          timeout -k 10 300 env $e $(cmd_for "$w") "$@" > "$O/envab_${w}_${i}_$rep.log" 2>&1
+          rc=$?; [ $rc -eq 0 ] || { echo "envab $i rc=$rc"; tail -8 "$O/envab_${w}_${i}_$rep.log"; exit $rc; }
+          grep '^{' "$O/envab_${w}_${i}_$rep.log" | tail -1 | python3 -c "
+import json, sys
+d = json.loads(sys.stdin.read())
+r = d.get('roofline') or {}
+keys = [k for k in list(d) + list(r) if k.endswith('_ms') or k in ('value', 'msamples_s')]
+print('[${sets[$i]}]', {k: d.get(k, r.get(k)) for k in keys})" | tee -a "$O/envab_${w}.txt"
+        done
+      done
+      if [ "${STATS:-0}" = 1 ]; then
+        for i in "${!sets[@]}"; do
+          e="${sets[$i]}"; [ "$e" = base ] && e=""
+          # shellcheck disable=SC2086
+          (if [ -n "$e" ]; then export $e; fi; prof "envstats_${w}_$i" --kernel-trace --stats -- "$w" "$@") || exit 1
+        done
+      fi ;;
     final)
       run_pass tests x
       run_pass smoke x
