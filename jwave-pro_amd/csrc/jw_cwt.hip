@@ -270,6 +270,20 @@ struct CoefOut {  // out[pair][t] = v / N for t = line + N1 * idx < n  (reverse 
   __device__ CoefRow bind(long item) const {  // fft::bind_out: the pair looked up once per line
     return CoefRow{out + 2 * pm.out_pair(pair0 + item) * n, n, N1, inv_n, nt};
   }
+  // the band kernel's output for (launch item, signal, scale): coefficient row sig * ns + s
+  __device__ CoefOut at(long, long sig, int s) const {
+    CoefOut o = *this;
+    o.pair0 = sig * pm.ns + s;
+    return o;
+  }
+};
+// The band kernel run on a coarse grid (cwt_interp below): row `item` of the workspace U
+// (M complex per launch item, natural order), unscaled, plain stores (U is read back next).
+struct CoarseOut {
+  double* U;
+  long M, N1, row;
+  __device__ CoarseOut at(long item, long, int) const { return CoarseOut{U, M, N1, item}; }
+  __device__ CoefRow bind(long) const { return CoefRow{U + 2 * row * M, M, N1, 1.0, false}; }
 };
 
 
@@ -286,10 +300,12 @@ struct CoefOut {  // out[pair][t] = v / N for t = line + N1 * idx < n  (reverse 
 constexpr double kBandE = 60.0;  // bins with |psi_hat| < e^-60 |psi_hat|max are dropped
 
 struct BandScale {
-  long b0;       // first 512-bin block of the band (mod N1)
+  long b0;       // first 512-bin block of the band (mod N1) in the transform's own spectrum
   long psi_off;  // offset of this scale's psi_hat band in the table (nb x 512 entries)
   int nb;        // blocks in the band
   int s;         // scale index
+  long fb0;      // first block in the signal's spectrum (mod Nx / 512): b0 unless coarse
+  long kc;       // coarse grid (cwt_interp): signed bin of the signal's spectrum at coarse bin 0
 };
 
 // psi_hat of every bin of every band block, as the two-pass path evaluates it (psi_bin)
@@ -325,11 +341,13 @@ typedef double d4v __attribute__((ext_vector_type(4)));
 // MF: band sums on the matrix cores (else VALU, Gauss form); PF: the next block pair's loads
 // issued before the current pair's MFMAs; WPE: waves per SIMD the registers are fitted to (6 =
 // three workgroups per CU, one row group each; 4 = two, R row groups each).
-template <bool MF, bool PF, int WPE>
+// Out: CoefOut (the coefficients) or CoarseOut (a coarse-grid transform for cwt_interp, where
+// N = M is the coarse length and the band is read from the signal's spectrum of length Nx).
+template <bool MF, bool PF, int WPE, class Out>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void cwt_band512(
     const cplx* __restrict__ Xn, const double* __restrict__ psi,
     const BandScale* __restrict__ bands, int nband, const double4* __restrict__ wN1, long N,
-    long N1, long items, CoefOut out, Tables T, int R) {
+    long N1, long items, Out out, Tables T, int R, long Nx) {
   __shared__ double tile[fft::kTileD];  // re/im-split staging (36.9 KB)
   // 32-bit index math (the scalar unit runs 64-bit division as a ~100-instruction sequence)
   const unsigned lrpp = (unsigned)__builtin_ctzl(N1 / (fft::kT * R)), local = blockIdx.x >> 3;
@@ -348,7 +366,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
   __syncthreads();  // the previous group's staging reads are done with the tile
   // thread (h, kp): columns kp and kp + 256, rows r0 + 4h .. r0 + 4h + 3 (h uniform per wave,
   // so each wave-uniform twiddle feeds two columns)
-  const unsigned m1 = (unsigned)N1 - 1;
+  const unsigned m1 = (unsigned)N1 - 1, mx = (unsigned)(Nx >> 9) - 1;
   if constexpr (!MF) {
   const int h = tid >> 8, kp = tid & 255;
   const unsigned rr = __builtin_amdgcn_readfirstlane((unsigned)r0 + 4 * h);  // wave-uniform
@@ -359,7 +377,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
   for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int q = 0; q < 2; ++q) s1[q][t] = s2[q][t] = s3[q][t] = 0.0;
-  const cplx* xs = Xn + (long)sig * N + kp;
+  const cplx* xs = Xn + (long)sig * Nx + kp;
   const double* ps = psi + b.psi_off + kp;
   constexpr int kU = 4;  // blocks whose loads are in flight together
   for (int j0 = 0; j0 < b.nb; j0 += kU) {
@@ -368,9 +386,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int j = j0 + u < b.nb ? j0 + u : b.nb - 1;  // clamped; skipped below
-      const unsigned k1 = ((unsigned)b.b0 + j) & m1;
-      xv[u][0] = xs[512 * k1];
-      xv[u][1] = xs[512 * k1 + 256];
+      const unsigned kx = ((unsigned)b.fb0 + j) & mx;
+      xv[u][0] = xs[512 * kx];
+      xv[u][1] = xs[512 * kx + 256];
       p[u][0] = ps[512 * j];
       p[u][1] = ps[512 * j + 256];
     }
@@ -427,7 +445,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q] = d4v{0.0, 0.0, 0.0, 0.0};
   // each lane loads only the part of Z it feeds (re for kq even, im for kq odd): 8-byte loads
-  const double* xs = (const double*)(Xn + (long)sig * N + 64 * c + tr) + zc;
+  const double* xs = (const double*)(Xn + (long)sig * Nx + 64 * c + tr) + zc;
   const double* ps = psi + b.psi_off + 64 * c + tr;
   // loads of the next block pair are issued before the current pair's MFMAs (the L2 latency of
   // one pair hides under the other's arithmetic); past the band the index clamps to nb - 1 and
@@ -436,14 +454,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const int j = j0 + jo;
     const bool in = j < b.nb;
     const int jj = in ? j : b.nb - 1;
-    const unsigned k1 = ((unsigned)b.b0 + jj) & m1;
+    const unsigned k1 = ((unsigned)b.b0 + jj) & m1, kx = ((unsigned)b.fb0 + jj) & mx;
     const double4 w = wN1[(k1 * ((unsigned)r0 + t)) & m1];
     // A[tr][kq]: Re row: (Re W, -Im W) for (Re Z, Im Z); Im row: (Im W, Re W)
     av = im_row ? (zc ? w.x : w.y) : (zc ? -w.y : w.x);
     av = in ? av : 0.0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      xv[q] = xs[2 * (512L * k1 + 16 * q)];
+      xv[q] = xs[2 * (512L * kx + 16 * q)];
       pv[q] = ps[512 * jj + 16 * q];
     }
   };
@@ -503,9 +521,112 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
   for (int r = 0; r < 8; ++r) a[r].y = tile[c * 512 + lane + 64 * r];
   __syncthreads();
-  CoefOut o = out;
-  o.pair0 = (long)sig * out.pm.ns + b.s;  // one output pair per workgroup
+  const Out o = out.at(item, sig, b.s);  // one output row per workgroup
   fft::pass512_tail_split<1, false>(a, o, N, 512L, T, 0L, r0, tile);
+  }
+}
+
+
+// ---------------------------------------------------------------------------------------
+// Band scales on a coarse grid.  A scale whose band (signed bins lo .. hi, centred on the
+// 512-aligned bin kc) fits in |m| <= M/4 of an M-point spectrum, M = N / P, gives
+//   y[t] = (1/N) sum_k Z[k] e^{2 pi i k t / N} = e^{2 pi i kc t / N} f(t / P) / N,
+//   f(tau) = sum_m Z[kc + m] e^{2 pi i m tau / M}      (a band-limited, M-periodic function),
+// and f is interpolated from the coarse samples u[s] = sum_m (Z[kc + m] / Phi(m / M)) e^{2 pi i m s / M}
+// (an M-point inverse DFT, run by the band kernel on the coarse grid) with a Kaiser-Bessel kernel
+// phi of width W: f(tau) = sum_s u[s] phi(tau - s) up to the kernel's aliasing, Phi being phi's
+// Fourier transform (the deconvolution; Jackson et al. 1991).  Oversampling M >= 4 |m|max with
+// W = 14 bounds that error near 1e-14 of the scale's peak (tests/test_cwt_gpu.py).  The coarse
+// transform is P times smaller than the scale's N-point one; the interpolation reads it from L2
+// and writes each coefficient once, in 1 KB pieces per wave.
+// ---------------------------------------------------------------------------------------
+constexpr int kInterpW = 14;     // kernel width (coarse samples)
+constexpr int kInterpTaps = 15;  // taps per output: s0 - 7 .. s0 + 7
+constexpr double kInterpBeta = 32.870457014757026;  // pi sqrt((W/2)^2 1.5^2 - 0.8), sigma = 2
+
+// Phi(nu) = W sinh(sqrt(beta^2 - (pi W nu)^2)) / sqrt(...), the transform of
+// phi(x) = I0(beta sqrt(1 - (2x/W)^2)), |x| <= W/2 (|nu| <= 1/2 here, so the root is real)
+__device__ __forceinline__ double kb_phi_hat(double nu) {
+  const double a = kPi * kInterpW * nu;
+  const double q = sqrt(kInterpBeta * kInterpBeta - a * a);
+  return kInterpW * sinh(q) / q;
+}
+
+// psi_hat of every bin of every band block (as psi_bin evaluates it) divided by Phi at the bin's
+// coarse frequency m / M, m = kk - kc
+template <int K>
+__global__ __launch_bounds__(256) void cwt_interp_psi(const BandScale* bands, double* psi,
+                                                      WaveletFT w, const double* scales,
+                                                      const double* sc, long N, long N1, double fs,
+                                                      long M) {
+  const BandScale b = bands[blockIdx.y];
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long)b.nb * 512) return;
+  const long k = 512 * ((b.fb0 + (e >> 9)) & (N1 - 1)) + (e & 511);
+  const long kk = k > N / 2 ? k - N : k;
+  psi[b.psi_off + e] = psi_bin<K>(w, scales, sc, b.s, k, N, fs).x / kb_phi_hat((double)(kk - b.kc) / (double)M);
+}
+
+// One workgroup = kInterpTC consecutive coefficients t of one (signal, scale) pair from its
+// coarse row U[item] (M = N / 2^LOGP samples).  The coarse samples the chunk needs are staged
+// in LDS; lane l of wave v takes t = t0 + v kInterpTC / 4 + l + 64 i, so its r = t mod P is fixed
+// (P <= 64) and its 15 weights phi(r / P + 7 - k) / N (wtab, host-made) stay in registers; the
+// lanes of one s0 = t / P read the same samples (LDS broadcast).  The phase e^{2 pi i kc t / N}
+// is one table lookup per lane, then a wave-uniform step per 64 outputs.
+constexpr int kInterpTC = 4096;
+template <int LOGP>
+__global__ __launch_bounds__(256) void cwt_interp(const cplx* __restrict__ U, long M,
+                                                  const BandScale* __restrict__ bands, int nsc,
+                                                  const double* __restrict__ wtab, long N, long n,
+                                                  int ns, long sig0, double* __restrict__ out,
+                                                  bool nt, Tables T, int chunks) {
+  constexpr int P = 1 << LOGP, NU = kInterpTC / P + 16, PER = kInterpTC / 4 / 64;
+  __shared__ cplx us[NU];
+  const unsigned bid = blockIdx.x, item = bid / (unsigned)chunks;
+  const unsigned chunk = bid - item * (unsigned)chunks;
+  const unsigned sl = item / (unsigned)nsc;
+  const BandScale b = bands[item - sl * (unsigned)nsc];
+  const long t0 = (long)chunk * kInterpTC;
+  const cplx* u = U + (long)item * M;
+  const long s_lo = (t0 >> LOGP) - 7;  // first staged sample (mod M)
+  for (int j = threadIdx.x; j < NU; j += 256) {
+    long q = s_lo + j;
+    q = q < 0 ? q + M : (q >= M ? q - M : q);
+    us[j] = u[q];
+  }
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long tl = t0 + (long)wv * (kInterpTC / 4) + lane;  // this lane's first output
+  const int r = (int)(tl & (P - 1));
+  double wr[kInterpTaps];
+#pragma unroll
+  for (int k = 0; k < kInterpTaps; ++k) wr[k] = wtab[r * 16 + k];
+  const long kcu = ((b.kc % N) + N) % N;
+  cplx ph = fft::twiddle(T, (kcu * tl) & (N - 1));
+  const cplx st = fft::twiddle(T, (kcu * 64) & (N - 1));
+  double* row = out + 2 * ((sig0 + sl) * ns + b.s) * n;
+  __syncthreads();
+  const int base0 = (int)((tl >> LOGP) - (t0 >> LOGP));
+#pragma unroll 4
+  for (int i = 0; i < PER; ++i) {
+    const long t = tl + 64 * i;
+    const int base = base0 + ((64 * i) >> LOGP);
+    double ar = 0.0, ai = 0.0;
+#pragma unroll
+    for (int k = 0; k < kInterpTaps; ++k) {
+      const cplx v = us[base + k];
+      ar = __builtin_fma(wr[k], v.x, ar);
+      ai = __builtin_fma(wr[k], v.y, ai);
+    }
+    const cplx y = fft::cmul(make_double2(ar, ai), ph);
+    if (t < n) {
+      cplx* o = (cplx*)(row + 2 * t);
+      if (nt) {
+        fft::nt_store(o, y);
+      } else {
+        *o = y;
+      }
+    }
+    ph = fft::cmul(ph, st);
   }
 }
 
@@ -590,6 +711,53 @@ static bool cwt_band(int wavelet, const WaveletFT& w, double a, double fs, long 
   return true;
 }
 
+// The coarse grid of a band (signed bins lo .. hi of the N-point spectrum) for cwt_interp:
+// centre kc on a 512-bin block boundary (so the coarse blocks are the signal's blocks), and the
+// smallest power of two M >= 4096 with the band inside |m| <= M/4 (oversampling 2: the
+// interpolation error bound of kInterpW) and its whole 512-bin blocks inside [-M/2, M/2).
+// cb0 = the band's first block on the coarse grid (mod M / 512).  P = N / M <= 64 (the
+// interpolation kernel's lane mapping).
+static bool coarse_grid(double lo, double hi, long N, long* M_out, long* kc_out, long* cb0) {
+  const long blo = (long)std::floor(lo / 512.0), bhi = (long)std::floor(hi / 512.0);
+  long s2 = blo + bhi + 1;  // floor((blo + bhi + 1) / 2)
+  const long kcb = s2 >= 0 ? s2 / 2 : -((-s2 + 1) / 2);
+  const long kc = 512 * kcb;
+  const double hw = std::max((double)kc - lo, hi - (double)kc);
+  long M = std::max(4096L, N / 64);
+  while (M <= N && ((double)M < 4.0 * hw || 512 * (kcb - blo) > M / 2 || 512 * (bhi + 1 - kcb) > M / 2))
+    M <<= 1;
+  if (M > N / 2) return false;
+  const long n1 = M / 512;
+  *M_out = M;
+  *kc_out = kc;
+  *cb0 = (((blo - kcb) % n1) + n1) % n1;
+  return true;
+}
+
+struct CoarseGroup {
+  long M;
+  int first, n, nb_hi;
+};
+
+// phi(x) / N at x = r / P + (taps / 2) - k for r < P, k < 16 (zero outside |x| <= W / 2):
+// the interpolation weights of cwt_interp, phi(x) = I0(beta sqrt(1 - (2x/W)^2))
+static void interp_weights(long P, long N, std::vector<double>& wt) {
+  wt.assign((size_t)P * 16, 0.0);
+  for (long r = 0; r < P; ++r)
+    for (int k = 0; k < kInterpTaps; ++k) {
+      const long double x = (long double)r / P + (kInterpTaps / 2) - k;
+      const long double z = 1.0L - (2.0L * x / kInterpW) * (2.0L * x / kInterpW);
+      if (z < 0) continue;
+      const long double b = (long double)kInterpBeta * std::sqrt(z), q = b * b / 4.0L;
+      long double term = 1.0L, sum = 1.0L;  // I0(b) = sum (b^2/4)^j / (j!)^2
+      for (int j = 1; j < 200 && term > sum * 1e-22L; ++j) {
+        term *= q / ((long double)j * j);
+        sum += term;
+      }
+      wt[(size_t)r * 16 + k] = (double)(sum / (long double)N);
+    }
+}
+
 // Group sizes: signals per forward chunk and (signal, scale) pairs per inverse group, so the
 // workspace A stays ~128 MB (Infinity Cache sized) at N = 2^18.
 int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
@@ -635,24 +803,58 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   // rest through the two-pass FFT.  One pass costs ~1.1 us per (signal, scale) pair at N = 2^18
   // plus ~0.05 us per block, two passes ~3 us: the measured optimum at cfg3 is nbmax = 32
   // (profiles/r02/cwt_band_sweep_r02.log).  env JW_CWT_BAND (A/B runs): nbmax, 0 = all two-pass.
+  // Before either, a band scale whose band fits a coarse grid of M = N / P points with P >=
+  // pmin runs there (cwt_interp): env JW_CWT_INTERP (A/B runs and tests) = pmin, 0 = never.
   const char* gbd = std::getenv("JW_CWT_BAND");
   const int nbmax = gbd ? std::atoi(gbd) : 32;
+  const char* gip = std::getenv("JW_CWT_INTERP");
+  const long pmin = gip ? std::atol(gip) : 4;
   const long N1b = N / 512;
-  std::vector<BandScale> bands;
+  std::vector<BandScale> bands, coarse;  // coarse: sorted by M below
+  std::vector<long> coarse_m;
   std::vector<int> full;
   long psi_total = 0;
   int nb_hi = 0;
   for (int i = 0; i < ns; ++i) {
     long b0 = 0;
     int nb = 0;
-    if (N >= 8192 && nbmax > 0 && cwt_band(wavelet, w, scales_host[i], fs, N, &b0, &nb) &&
-        nb <= nbmax && nb <= N1b) {
-      bands.push_back(BandScale{b0, psi_total, nb, i});
+    double lo = 0.0, hi = 0.0;
+    const bool bandok = N >= 8192 && cwt_band(wavelet, w, scales_host[i], fs, N, &b0, &nb, &lo, &hi) &&
+                        nb <= N1b;
+    if (bandok && pmin > 0) {
+      long M = 0, kc = 0, cb0 = 0;
+      if (coarse_grid(lo, hi, N, &M, &kc, &cb0) && M <= N / pmin) {
+        coarse.push_back(BandScale{cb0, 0, nb, i, b0, kc});
+        coarse_m.push_back(M);
+        continue;
+      }
+    }
+    if (bandok && nbmax > 0 && nb <= nbmax) {
+      bands.push_back(BandScale{b0, psi_total, nb, i, b0, 0});
       psi_total += 512L * nb;
       nb_hi = std::max(nb_hi, nb);
     } else {
       full.push_back(i);
     }
+  }
+  // coarse scales grouped by M (one band-kernel and one interpolation launch per group)
+  std::vector<CoarseGroup> groups;
+  {
+    std::vector<int> ord(coarse.size());
+    for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return coarse_m[a] < coarse_m[b]; });
+    std::vector<BandScale> sorted;
+    for (int k : ord) {
+      BandScale b = coarse[k];
+      b.psi_off = psi_total;
+      psi_total += 512L * b.nb;
+      if (groups.empty() || groups.back().M != coarse_m[k])
+        groups.push_back(CoarseGroup{coarse_m[k], (int)sorted.size(), 0, 0});
+      groups.back().n++;
+      groups.back().nb_hi = std::max(groups.back().nb_hi, b.nb);
+      sorted.push_back(b);
+    }
+    coarse = std::move(sorted);
   }
   const int nband = (int)bands.size(), nfull = (int)full.size();
   const char* gmb = std::getenv("JW_CWT_GROUP_MB");  // A/B runs: workspace size in MiB
@@ -696,12 +898,44 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   }
   JW_HIP_TRY(mem.alloc(&dsc, hsc.size() * sizeof(double)));
   JW_HIP_TRY(upload_async(dsc, hsc.data(), hsc.size() * sizeof(double), s));
-  if (nband > 0) {
+  BandScale* dcoarse = nullptr;
+  if (nband > 0 || !coarse.empty()) {
     JW_HIP_TRY(mem.alloc(&Xn, (size_t)batch * N * sizeof(cplx)));
     JW_HIP_TRY(mem.alloc(&psi, (size_t)psi_total * sizeof(double)));
+  }
+  if (nband > 0) {
     JW_HIP_TRY(mem.alloc(&wN1, (size_t)N1b * sizeof(double4)));
     JW_HIP_TRY(mem.alloc(&dbands, bands.size() * sizeof(BandScale)));
     JW_HIP_TRY(upload_async(dbands, bands.data(), bands.size() * sizeof(BandScale), s));
+  }
+  // coarse-grid workspaces (allocated and filled here, on the caller's stream, before the band
+  // stream forks): U ~128 MB of coarse rows (gchunk signals of a group at a time), the
+  // interpolation weights of each group's P, the row roots of each group's M
+  cplx* U = nullptr;
+  double* dwt = nullptr;
+  double4* wroots = nullptr;
+  std::vector<long> gchunk(groups.size());
+  std::vector<Tables> gT(groups.size());
+  for (size_t g = 0; g < groups.size(); ++g)
+    if ((st = fft::tables(groups[g].M, &gT[g])) != JW_OK) return st;
+  if (!coarse.empty()) {
+    JW_HIP_TRY(mem.alloc(&dcoarse, coarse.size() * sizeof(BandScale)));
+    JW_HIP_TRY(upload_async(dcoarse, coarse.data(), coarse.size() * sizeof(BandScale), s));
+    long ubytes = 0, rtot = 0;
+    std::vector<double> hwt;
+    for (size_t g = 0; g < groups.size(); ++g) {
+      const long per_sig = (long)groups[g].n * groups[g].M * (long)sizeof(cplx);
+      gchunk[g] = std::max(1L, std::min<long>(batch, (128L << 20) / per_sig));
+      ubytes = std::max(ubytes, gchunk[g] * per_sig);
+      rtot += groups[g].M / 512;
+      std::vector<double> wt;
+      interp_weights(N / groups[g].M, N, wt);
+      hwt.insert(hwt.end(), wt.begin(), wt.end());
+    }
+    JW_HIP_TRY(mem.alloc(&U, (size_t)ubytes));
+    JW_HIP_TRY(mem.alloc(&dwt, hwt.size() * sizeof(double)));
+    JW_HIP_TRY(mem.alloc(&wroots, (size_t)rtot * sizeof(double4)));
+    JW_HIP_TRY(upload_async(dwt, hwt.data(), hwt.size() * sizeof(double), s));
   }
   if (nfull > 0 && nfull < ns) {
     JW_HIP_TRY(mem.alloc(&dsmap, full.size() * sizeof(int)));
@@ -723,18 +957,33 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
       st = run_fft<-1>(N, nb, in, SpecOut1{X, N, b0}, so, A, s, T, (ntm & 1) != 0);
     }
   }
+  // with two-pass pairs to follow, the band and coarse-grid scales run on the side stream beside
+  // them (env JW_CWT_OVERLAP=0: one after the other, A/B runs)
+  hipStream_t bs = s;
+  if (st == JW_OK && (nband > 0 || !coarse.empty()) && pairs > 0) {
+    const char* gov = std::getenv("JW_CWT_OVERLAP");
+    if (!(gov && gov[0] == '0')) {
+      SideStream* side = nullptr;
+      if ((st = side_stream(&side)) != JW_OK) return st;
+      JW_HIP_TRY(hipEventRecord(side->fork, s));
+      bs = side->s;
+      JW_HIP_TRY(hipStreamWaitEvent(bs, side->fork, 0));
+      join.side = side;  // armed before the launches: any exit below joins
+    }
+  }
   // band scales: one pass per (signal, scale) pair
   if (nband > 0 && st == JW_OK) {
     const dim3 gp((unsigned)((nb_hi * 512L + 255) / 256), (unsigned)nband);
+    // (on the band stream: it forked before these tables)
     if (wavelet == JW_CWT_MORLET) {
-      hipLaunchKernelGGL(cwt_band_psi<JW_CWT_MORLET>, gp, dim3(256), 0, s, dbands, psi, w, dsc,
+      hipLaunchKernelGGL(cwt_band_psi<JW_CWT_MORLET>, gp, dim3(256), 0, bs, dbands, psi, w, dsc,
                          dsc + ns, N, N1b, fs);
     } else {
-      hipLaunchKernelGGL(cwt_band_psi<JW_CWT_MEXHAT>, gp, dim3(256), 0, s, dbands, psi, w, dsc,
+      hipLaunchKernelGGL(cwt_band_psi<JW_CWT_MEXHAT>, gp, dim3(256), 0, bs, dbands, psi, w, dsc,
                          dsc + ns, N, N1b, fs);
     }
     JW_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(cwt_band_roots, dim3((unsigned)((N1b + 255) / 256)), dim3(256), 0, s, wN1,
+    hipLaunchKernelGGL(cwt_band_roots, dim3((unsigned)((N1b + 255) / 256)), dim3(256), 0, bs, wN1,
                        N, N1b, T);
     JW_HIP_TRY(hipGetLastError());
     const CoefOut ob{out, n, N1b, 0, 1.0 / (double)N, (ntm & 2) != 0, pm_all};
@@ -752,36 +1001,81 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     const long blocks = (items + 7) / 8 * 8 * (N1b / fft::kT / R);
     if (blocks > 0x7fffffffL) return fail(JW_ERR_UNSUPPORTED, "CWT band grid too large");
     const char* gmf = std::getenv("JW_CWT_BAND_MFMA");
-    // with two-pass pairs to follow, the band kernel runs on the side stream beside them
-    // (env JW_CWT_OVERLAP=0: one after the other, A/B runs)
-    const char* gov = std::getenv("JW_CWT_OVERLAP");
-    hipStream_t bs = s;
-    if (pairs > 0 && !(gov && gov[0] == '0')) {
-      SideStream* side = nullptr;
-      if ((st = side_stream(&side)) != JW_OK) return st;
-      JW_HIP_TRY(hipEventRecord(side->fork, s));
-      bs = side->s;
-      JW_HIP_TRY(hipStreamWaitEvent(bs, side->fork, 0));
-      join.side = side;  // armed before the launch: any exit below joins
-    }
     auto band = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(512), 0, bs, Xn, psi, dbands, nband,
-                         wN1, N, N1b, items, ob, T, R);
+                         wN1, N, N1b, items, ob, T, R, N);
     };
     if (gmf && gmf[0] == '0') {
-      band(cwt_band512<false, false, 4>);
+      band(cwt_band512<false, false, 4, CoefOut>);
     } else if (bv == 0) {
-      band(cwt_band512<true, false, 4>);
+      band(cwt_band512<true, false, 4, CoefOut>);
     } else if (bv == 1) {
-      band(cwt_band512<true, true, 4>);
+      band(cwt_band512<true, true, 4, CoefOut>);
     } else if (bv == 2) {
-      band(cwt_band512<true, false, 6>);
+      band(cwt_band512<true, false, 6, CoefOut>);
     } else {
-      band(cwt_band512<true, true, 6>);
+      band(cwt_band512<true, true, 6, CoefOut>);
     }
     JW_HIP_TRY(hipGetLastError());
-    if (join.side) JW_HIP_TRY(hipEventRecord(join.side->join, bs));
   }
+  // coarse-grid scales: per group of equal M, the band kernel on the M-point grid into U, then
+  // the Kaiser-Bessel interpolation to the N-point coefficients, a few signals at a time so
+  // that U stays ~128 MB
+  if (!groups.empty() && st == JW_OK) {
+    const bool nt = (ntm & 2) != 0;
+    long woff = 0, roff = 0;
+    for (size_t g = 0; g < groups.size() && st == JW_OK; ++g) {
+      const CoarseGroup& G = groups[g];
+      const long M = G.M, N1c = M / 512, P = N / M;
+      const Tables& TM = gT[g];
+      const BandScale* gb = dcoarse + G.first;
+      const dim3 gp((unsigned)((G.nb_hi * 512L + 255) / 256), (unsigned)G.n);
+      if (wavelet == JW_CWT_MORLET) {
+        hipLaunchKernelGGL(cwt_interp_psi<JW_CWT_MORLET>, gp, dim3(256), 0, bs, gb, psi, w, dsc,
+                           dsc + ns, N, N1b, fs, M);
+      } else {
+        hipLaunchKernelGGL(cwt_interp_psi<JW_CWT_MEXHAT>, gp, dim3(256), 0, bs, gb, psi, w, dsc,
+                           dsc + ns, N, N1b, fs, M);
+      }
+      JW_HIP_TRY(hipGetLastError());
+      double4* wN1c = wroots + roff;
+      hipLaunchKernelGGL(cwt_band_roots, dim3((unsigned)((N1c + 255) / 256)), dim3(256), 0, bs,
+                         wN1c, M, N1c, TM);
+      JW_HIP_TRY(hipGetLastError());
+      const double* gw = dwt + woff;
+      woff += P * 16;
+      roff += N1c;
+      const int chunks = (int)((n + kInterpTC - 1) / kInterpTC);
+      for (long sg0 = 0; sg0 < batch; sg0 += gchunk[g]) {
+        const long cs = std::min<long>(gchunk[g], batch - sg0);
+        const long items = cs * G.n;
+        const long blocks = (items + 7) / 8 * 8 * (N1c / fft::kT);
+        const long iblocks = items * chunks;
+        if (blocks > 0x7fffffffL || iblocks > 0x7fffffffL)
+          return fail(JW_ERR_UNSUPPORTED, "CWT coarse grid too large");
+        hipLaunchKernelGGL((cwt_band512<true, true, 6, CoarseOut>), dim3((unsigned)blocks), dim3(512), 0,
+                           bs, Xn + sg0 * N, psi, gb, G.n, wN1c, M, N1c, items,
+                           CoarseOut{(double*)U, M, N1c, 0}, TM, 1, N);
+        JW_HIP_TRY(hipGetLastError());
+        auto interp = [&](auto lp) {
+          constexpr int LP = decltype(lp)::value;
+          hipLaunchKernelGGL(cwt_interp<LP>, dim3((unsigned)iblocks), dim3(256), 0, bs, U, M, gb,
+                             G.n, gw, N, n, ns, sg0, out, nt, T, chunks);
+        };
+        switch (P) {
+          case 1: interp(std::integral_constant<int, 0>{}); break;
+          case 2: interp(std::integral_constant<int, 1>{}); break;
+          case 4: interp(std::integral_constant<int, 2>{}); break;
+          case 8: interp(std::integral_constant<int, 3>{}); break;
+          case 16: interp(std::integral_constant<int, 4>{}); break;
+          case 32: interp(std::integral_constant<int, 5>{}); break;
+          default: interp(std::integral_constant<int, 6>{}); break;
+        }
+        JW_HIP_TRY(hipGetLastError());
+      }
+    }
+  }
+  if (join.side) JW_HIP_TRY(hipEventRecord(join.side->join, bs));
   // the other (signal, scale) pairs: IFFT(X * psi_hat) -> coefficients in two passes
   if (pipe && st == JW_OK) {
     auto go = [&](auto kind) {

@@ -144,6 +144,7 @@ def test_band_scales_one_pass(kind, n, monkeypatch):
     wv, params = {"morlet": (MorletWavelet(*MORLET6), MORLET6),
                   "mexhat": (MexicanHatWavelet(1.5), (1.5, 0.0))}[kind]
     x = orc.fill_uniform(n, 5)
+    monkeypatch.setenv("JW_CWT_INTERP", "0")  # no coarse grids: the band kernel itself
     monkeypatch.setenv("JW_CWT_BAND", "1000")
     band = CWT(wv).transformFFT(x, scales, 1.0).getCoefficients()
     monkeypatch.setenv("JW_CWT_BAND", "0")
@@ -153,6 +154,34 @@ def test_band_scales_one_pass(kind, n, monkeypatch):
     assert nw(band, ex) < TOL_EXACT
     for i in range(len(scales)):  # per scale, against that scale's own magnitude
         assert nw(band[i], ex[i]) < 1e-11, (i, nw(band[i], ex[i]))
+
+
+@pytest.mark.parametrize("kind", ["morlet", "mexhat"])
+@pytest.mark.parametrize("n", [1 << 14, 1 << 16, 1 << 18, 300001, 1 << 20])
+@pytest.mark.parametrize("pmin", ["4", "2"])
+def test_coarse_grid_scales(kind, n, pmin, monkeypatch):
+    # Band scales whose band fits a grid of M = N / P points (P >= JW_CWT_INTERP) run as an
+    # M-point inverse DFT (the band kernel on the coarse grid, the band divided by the
+    # Kaiser-Bessel kernel's transform) and a 15-tap interpolation to the N-point coefficients.
+    # Against the same scales through the two-pass FFT (JW_CWT_INTERP=0, JW_CWT_BAND=0): the
+    # interpolation error is ~1e-14 of each scale's peak (W = 14, oversampling 2); against the
+    # oracle per scale as the other paths.  pmin = 2 also runs the P = 2 grids.
+    scales = CWT.generateLogScales(2.0, 1024.0, 14)
+    wv, params = {"morlet": (MorletWavelet(*MORLET6), MORLET6),
+                  "mexhat": (MexicanHatWavelet(1.5), (1.5, 0.0))}[kind]
+    x = orc.fill_uniform(n, 11)
+    monkeypatch.setenv("JW_CWT_INTERP", pmin)
+    got = CWT(wv).transformFFT(x, scales, 1.0).getCoefficients()
+    monkeypatch.setenv("JW_CWT_INTERP", "0")
+    monkeypatch.setenv("JW_CWT_BAND", "0")
+    two = CWT(wv).transformFFT(x, scales, 1.0).getCoefficients()
+    for i in range(len(scales)):
+        assert nw(got[i], two[i]) < 1e-12, (i, nw(got[i], two[i]))
+    if n <= (1 << 18):
+        ex = orc.cwt_fft(x, scales, 1.0, kind, params, 1, exact=True)
+        assert nw(got, ex) < TOL_EXACT
+        for i in range(len(scales)):
+            assert nw(got[i], ex[i]) < 1e-11, (i, nw(got[i], ex[i]))
 
 
 @pytest.mark.parametrize("kind", ["morlet", "mexhat"])
