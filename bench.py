@@ -31,9 +31,9 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "Msamples/s forward+inverse MODWT (db4, 8 levels, N=2^20); max recon error"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level table)
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "modwt_pmc_traffic.json")
-# cwt / fwt2d HBM bytes per step at their default configs (tools/pmc_traffic.sh,
-# tools/traffic_summary.py)
-TRAFFIC_STEP_FILE = os.path.join(ROOT, "profiles", "r04", "final_z", "traffic_cwt_fwt2d.json")
+# cwt / fwt2d HBM bytes per step at their default configs (tools/evidence.sh TAG traffic W,
+# tools/summarize.py traffic)
+TRAFFIC_STEP_FILE = os.path.join(ROOT, "profiles", "r05", "traffic_cwt_fwt2d.json")
 
 
 def generate_inputs(gen, min_seconds=1.0):
@@ -289,10 +289,11 @@ def main_cwt(args, dev, rank, world):
                          "note": "one launch = one jw_cwt_fft call over the batch (all FFT "
                                  "passes); traffic = rocprofv3 FETCH_SIZE*2 + WRITE_SIZE per call "
                                  f"({os.path.relpath(TRAFFIC_STEP_FILE, ROOT)}): the A workspace round "
-                                 "trip of the two-pass scales is the excess over algorithmic; the "
-                                 "band scales (cwt_band512) run in one pass.  The structure's own "
-                                 "floor (34 two-pass scales at 3x their output, 30 one-pass) is "
-                                 "~142 GB per call (DESIGN.md 9c)"},
+                                 "trip of the 27 two-pass scales (a < 29) is the excess over "
+                                 "algorithmic; the 37 scales whose band fits a coarse grid of "
+                                 "N/P points (P >= 4) run as an M-point inverse DFT (cwt_band512 "
+                                 "on the coarse grid) plus a Kaiser-Bessel interpolation "
+                                 "(cwt_interp) that writes each coefficient once (DESIGN.md 5.4)"},
             "cpu_baseline": cpu}), flush=True)
 
 

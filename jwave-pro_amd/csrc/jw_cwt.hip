@@ -957,12 +957,16 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
       st = run_fft<-1>(N, nb, in, SpecOut1{X, N, b0}, so, A, s, T, (ntm & 1) != 0);
     }
   }
-  // with two-pass pairs to follow, the band and coarse-grid scales run on the side stream beside
-  // them (env JW_CWT_OVERLAP=0: one after the other, A/B runs)
+  // with two-pass pairs to follow, the band kernel (FP64-issue bound) runs on a side stream
+  // beside them; the coarse-grid scales go there too.  Without band scales nothing overlaps
+  // usefully: the coarse-grid kernels and the two-pass passes are all HBM-bound, and side by
+  // side cfg3 ran 32.0 ms against 30.6 one after the other (profiles/r05/ab/cwt_env_h.txt).
+  // env JW_CWT_OVERLAP (A/B runs): 0 = never, 1 = whenever there are pairs.
   hipStream_t bs = s;
+  const char* gov = std::getenv("JW_CWT_OVERLAP");
+  const bool overlap = gov ? gov[0] != '0' : nband > 0;
   if (st == JW_OK && (nband > 0 || !coarse.empty()) && pairs > 0) {
-    const char* gov = std::getenv("JW_CWT_OVERLAP");
-    if (!(gov && gov[0] == '0')) {
+    if (overlap) {
       SideStream* side = nullptr;
       if ((st = side_stream(&side)) != JW_OK) return st;
       JW_HIP_TRY(hipEventRecord(side->fork, s));

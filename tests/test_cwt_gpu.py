@@ -260,13 +260,15 @@ def test_fft_scalogram_fused(device):
     assert np.array_equal(t.transformFFTScalogram(np.zeros((2, 0)), scales), np.zeros((2, 11)))
 
 
-def test_concurrent_host_threads_with_side_streams():
+def test_concurrent_host_threads_with_side_streams(monkeypatch):
     # Host arrays (JW_HOST) from four threads at once: each thread stages on its own streams
-    # and runs its band scales on its own side stream (forked from and joined into its staging
-    # stream).  Every thread's result equals the same call made alone, bit for bit, and with
-    # the side stream off (JW_CWT_OVERLAP=0: the same kernels on one stream).
+    # and runs its band and coarse-grid scales on its own side stream (forked from and joined
+    # into its staging stream; JW_CWT_OVERLAP=1 forces the side stream, which by default only
+    # band-kernel scales take).  Every thread's result equals the same call made alone, bit for
+    # bit, and with the side stream off (JW_CWT_OVERLAP=0: the same kernels on one stream).
     import os
     import threading
+    monkeypatch.setenv("JW_CWT_OVERLAP", "1")
     n = 1 << 16
     scales = CWT.generateLogScales(2.0, 1024.0, 16)
     xs = [orc.fill_uniform(n, 100 + i) for i in range(4)]
@@ -291,10 +293,7 @@ def test_concurrent_host_threads_with_side_streams():
     for i in range(4):
         assert np.array_equal(got[i], alone[i]), i
     os.environ["JW_CWT_OVERLAP"] = "0"
-    try:
-        one = CWT(MorletWavelet(*MORLET6)).transformFFT(xs[0], scales, 1.0).getCoefficients()
-    finally:
-        del os.environ["JW_CWT_OVERLAP"]
+    one = CWT(MorletWavelet(*MORLET6)).transformFFT(xs[0], scales, 1.0).getCoefficients()
     assert np.array_equal(one, alone[0])
 
 
