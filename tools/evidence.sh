@@ -15,7 +15,9 @@
 #                     rounds; STATS=1 adds a kernel trace per setting)
 #             final   tests, smoke, bench_all, then stats + traffic of modwt and cwt
 #   WORKLOAD  modwt (headline, default) | sym8 (cfg5) | cwt (cfg3) | fwt2d (cfg4) |
-#             auto (JWave's default path: AUTO STRICT db4 J=8, 128 x 2^20, tools/modwt_time.py)
+#             auto (JWave's default path: AUTO STRICT db4 J=8, 128 x 2^20, tools/modwt_time.py) |
+#             fft (JWave's FFT alone, 128 x 2^20, tools/fft_time.py; JW_JFFT_3PASS_MIN=1048576 for
+#             the three-pass split)
 # Output: gpurun_out/TAG/ (copy what is judged into profiles/rNN/).
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R" || exit 2
@@ -32,6 +34,7 @@ cmd_for() {  # the program one workload runs (after rocprofv3's --, or on its ow
     cwt)   echo "python3 $R/bench.py --workload cwt --no-cpu-baseline --no-check --steps 3 --warmup 1" ;;
     fwt2d) echo "python3 $R/bench.py --workload fwt2d --no-cpu-baseline --no-check --no-alt --steps 3 --warmup 1" ;;
     auto)  echo "python3 $R/tools/modwt_time.py --method auto --arith strict --batch 128 --reps 3" ;;
+    fft)   echo "python3 $R/tools/fft_time.py --n 1048576 --batch 128 --reps 3" ;;
     *) echo "unknown workload $1" >&2; exit 2 ;;
   esac
 }
