@@ -535,14 +535,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // and f is interpolated from the coarse samples u[s] = sum_m (Z[kc + m] / Phi(m / M)) e^{2 pi i m s / M}
 // (an M-point inverse DFT, run by the band kernel on the coarse grid) with a Kaiser-Bessel kernel
 // phi of width W: f(tau) = sum_s u[s] phi(tau - s) up to the kernel's aliasing, Phi being phi's
-// Fourier transform (the deconvolution; Jackson et al. 1991).  Oversampling M >= 4 |m|max with
-// W = 14 bounds that error near 1e-14 of the scale's peak (tests/test_cwt_gpu.py).  The coarse
-// transform is P times smaller than the scale's N-point one; the interpolation reads it from L2
-// and writes each coefficient once, in 1 KB pieces per wave.
+// Fourier transform (the deconvolution; Jackson et al. 1991).  Oversampling M >= 3 |m|max
+// (sigma = 1.5) with W = 16 bounds that error near 1e-14 of the scale's peak (numpy prototype
+// over the cfg3 scales: <= 1.7e-14; tests/test_cwt_gpu.py).  The coarse transform is P times
+// smaller than the scale's N-point one; the interpolation reads it from L2 and writes each
+// coefficient once, in 1 KB pieces per wave.
 // ---------------------------------------------------------------------------------------
-constexpr int kInterpW = 14;     // kernel width (coarse samples)
-constexpr int kInterpTaps = 15;  // taps per output: s0 - 7 .. s0 + 7
-constexpr double kInterpBeta = 32.870457014757026;  // pi sqrt((W/2)^2 1.5^2 - 0.8), sigma = 2
+constexpr int kInterpW = 16;                   // kernel width (coarse samples)
+constexpr int kInterpHalf = kInterpW / 2;
+constexpr int kInterpTaps = 2 * kInterpHalf + 1;  // taps per output: s0 - 8 .. s0 + 8
+constexpr int kInterpStride = 20;              // weights per r in the table
+constexpr double kInterpSigma = 1.5;           // minimum oversampling of the band on the grid
+// beta = pi sqrt((W / sigma)^2 (sigma - 1/2)^2 - 0.8) (Beatty et al. 2005)
+constexpr double kInterpBeta = 33.39230409511825;
 
 // Phi(nu) = W sinh(sqrt(beta^2 - (pi W nu)^2)) / sqrt(...), the transform of
 // phi(x) = I0(beta sqrt(1 - (2x/W)^2)), |x| <= W/2 (|nu| <= 1/2 here, so the root is real)
@@ -570,7 +575,7 @@ __global__ __launch_bounds__(256) void cwt_interp_psi(const BandScale* bands, do
 // One workgroup = kInterpTC consecutive coefficients t of one (signal, scale) pair from its
 // coarse row U[item] (M = N / 2^LOGP samples).  The coarse samples the chunk needs are staged
 // in LDS; lane l of wave v takes t = t0 + v kInterpTC / 4 + l + 64 i, so its r = t mod P is fixed
-// (P <= 64) and its 15 weights phi(r / P + 7 - k) / N (wtab, host-made) stay in registers; the
+// (P <= 64) and its 17 weights phi(r / P + 8 - k) / N (wtab, host-made) stay in registers; the
 // lanes of one s0 = t / P read the same samples (LDS broadcast).  The phase e^{2 pi i kc t / N}
 // is one table lookup per lane, then a wave-uniform step per 64 outputs.
 constexpr int kInterpTC = 4096;
@@ -580,7 +585,7 @@ __global__ __launch_bounds__(256) void cwt_interp(const cplx* __restrict__ U, lo
                                                   const double* __restrict__ wtab, long N, long n,
                                                   int ns, long sig0, double* __restrict__ out,
                                                   bool nt, Tables T, int chunks) {
-  constexpr int P = 1 << LOGP, NU = kInterpTC / P + 16, PER = kInterpTC / 4 / 64;
+  constexpr int P = 1 << LOGP, NU = kInterpTC / P + kInterpTaps, PER = kInterpTC / 4 / 64;
   __shared__ cplx us[NU];
   const unsigned bid = blockIdx.x, item = bid / (unsigned)chunks;
   const unsigned chunk = bid - item * (unsigned)chunks;
@@ -588,7 +593,7 @@ __global__ __launch_bounds__(256) void cwt_interp(const cplx* __restrict__ U, lo
   const BandScale b = bands[item - sl * (unsigned)nsc];
   const long t0 = (long)chunk * kInterpTC;
   const cplx* u = U + (long)item * M;
-  const long s_lo = (t0 >> LOGP) - 7;  // first staged sample (mod M)
+  const long s_lo = (t0 >> LOGP) - kInterpHalf;  // first staged sample (mod M)
   for (int j = threadIdx.x; j < NU; j += 256) {
     long q = s_lo + j;
     q = q < 0 ? q + M : (q >= M ? q - M : q);
@@ -599,7 +604,7 @@ __global__ __launch_bounds__(256) void cwt_interp(const cplx* __restrict__ U, lo
   const int r = (int)(tl & (P - 1));
   double wr[kInterpTaps];
 #pragma unroll
-  for (int k = 0; k < kInterpTaps; ++k) wr[k] = wtab[r * 16 + k];
+  for (int k = 0; k < kInterpTaps; ++k) wr[k] = wtab[r * kInterpStride + k];
   const long kcu = ((b.kc % N) + N) % N;
   cplx ph = fft::twiddle(T, (kcu * tl) & (N - 1));
   const cplx st = fft::twiddle(T, (kcu * 64) & (N - 1));
@@ -713,8 +718,8 @@ static bool cwt_band(int wavelet, const WaveletFT& w, double a, double fs, long 
 
 // The coarse grid of a band (signed bins lo .. hi of the N-point spectrum) for cwt_interp:
 // centre kc on a 512-bin block boundary (so the coarse blocks are the signal's blocks), and the
-// smallest power of two M >= 4096 with the band inside |m| <= M/4 (oversampling 2: the
-// interpolation error bound of kInterpW) and its whole 512-bin blocks inside [-M/2, M/2).
+// smallest power of two M >= 4096 with the band inside |m| <= M / (2 kInterpSigma) (the
+// oversampling the kernel's error bound assumes) and its whole 512-bin blocks inside [-M/2, M/2).
 // cb0 = the band's first block on the coarse grid (mod M / 512).  P = N / M <= 64 (the
 // interpolation kernel's lane mapping).
 static bool coarse_grid(double lo, double hi, long N, long* M_out, long* kc_out, long* cb0) {
@@ -724,7 +729,8 @@ static bool coarse_grid(double lo, double hi, long N, long* M_out, long* kc_out,
   const long kc = 512 * kcb;
   const double hw = std::max((double)kc - lo, hi - (double)kc);
   long M = std::max(4096L, N / 64);
-  while (M <= N && ((double)M < 4.0 * hw || 512 * (kcb - blo) > M / 2 || 512 * (bhi + 1 - kcb) > M / 2))
+  while (M <= N && ((double)M < 2.0 * kInterpSigma * hw || 512 * (kcb - blo) > M / 2 ||
+                     512 * (bhi + 1 - kcb) > M / 2))
     M <<= 1;
   if (M > N / 2) return false;
   const long n1 = M / 512;
@@ -739,13 +745,13 @@ struct CoarseGroup {
   int first, n, nb_hi;
 };
 
-// phi(x) / N at x = r / P + (taps / 2) - k for r < P, k < 16 (zero outside |x| <= W / 2):
-// the interpolation weights of cwt_interp, phi(x) = I0(beta sqrt(1 - (2x/W)^2))
+// phi(x) / N at x = r / P + kInterpHalf - k for r < P, k < kInterpTaps (zero outside |x| <=
+// W / 2): the interpolation weights of cwt_interp, phi(x) = I0(beta sqrt(1 - (2x/W)^2))
 static void interp_weights(long P, long N, std::vector<double>& wt) {
-  wt.assign((size_t)P * 16, 0.0);
+  wt.assign((size_t)P * kInterpStride, 0.0);
   for (long r = 0; r < P; ++r)
     for (int k = 0; k < kInterpTaps; ++k) {
-      const long double x = (long double)r / P + (kInterpTaps / 2) - k;
+      const long double x = (long double)r / P + kInterpHalf - k;
       const long double z = 1.0L - (2.0L * x / kInterpW) * (2.0L * x / kInterpW);
       if (z < 0) continue;
       const long double b = (long double)kInterpBeta * std::sqrt(z), q = b * b / 4.0L;
@@ -754,7 +760,7 @@ static void interp_weights(long P, long N, std::vector<double>& wt) {
         term *= q / ((long double)j * j);
         sum += term;
       }
-      wt[(size_t)r * 16 + k] = (double)(sum / (long double)N);
+      wt[(size_t)r * kInterpStride + k] = (double)(sum / (long double)N);
     }
 }
 
@@ -1047,7 +1053,7 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
                          wN1c, M, N1c, TM);
       JW_HIP_TRY(hipGetLastError());
       const double* gw = dwt + woff;
-      woff += P * 16;
+      woff += P * kInterpStride;
       roff += N1c;
       const int chunks = (int)((n + kInterpTC - 1) / kInterpTC);
       for (long sg0 = 0; sg0 < batch; sg0 += gchunk[g]) {
