@@ -279,11 +279,16 @@ struct CoefOut {  // out[pair][t] = v / N for t = line + N1 * idx < n  (reverse 
 };
 // The band kernel run on a coarse grid (cwt_interp below): row `item` of the workspace U
 // (M complex per launch item, natural order), unscaled, plain stores (U is read back next).
+struct CoarseRow {  // u[t], t = line + N1 idx < M: unscaled, every index in range
+  cplx* u;
+  long N1;
+  __device__ void operator()(long idx, long line, cplx v) const { u[line + N1 * idx] = v; }
+};
 struct CoarseOut {
   double* U;
   long M, N1, row;
   __device__ CoarseOut at(long item, long, int) const { return CoarseOut{U, M, N1, item}; }
-  __device__ CoefRow bind(long) const { return CoefRow{U + 2 * row * M, M, N1, 1.0, false}; }
+  __device__ CoarseRow bind(long) const { return CoarseRow{(cplx*)(U + 2 * row * M), N1}; }
 };
 
 
@@ -526,6 +531,125 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
 }
 
+
+// The band kernel for grids of N1 >= 16 rows, two row groups per workgroup: rows r0 .. r0 + 7
+// and r0 + N1/2 .. r0 + N1/2 + 7.  W_N1^(k1 (n1 + N1/2)) = (-1)^k1 W_N1^(k1 n1), so with the
+// band's sums split by the parity of the block index k1,
+//   A[n1] ~ S_even(n1) + S_odd(n1),   A[n1 + N1/2] ~ S_even(n1) - S_odd(n1),
+// the MFMAs of one row group give both (half the band-sum work per row).  Each MFMA takes two
+// blocks of one parity (j and j + 2).  MFMA only; one workgroup = 16 rows, 2 per CU (WPE 4).
+#ifndef JW_CWT_PAR_PF
+#define JW_CWT_PAR_PF 1
+#endif
+template <class Out>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void cwt_band512_par(
+    const cplx* __restrict__ Xn, const double* __restrict__ psi,
+    const BandScale* __restrict__ bands, int nband, const double4* __restrict__ wN1, long N,
+    long N1, long items, Out out, Tables T, long Nx) {
+  __shared__ double tile[fft::kTileD];
+  const unsigned lrpp = (unsigned)__builtin_ctzl(N1 / (2 * fft::kT)), local = blockIdx.x >> 3;
+  const unsigned slot = local >> lrpp;
+  const unsigned item = slot * 8 + (blockIdx.x & 7);
+  const unsigned rg = local - (slot << lrpp);
+  if (item >= (unsigned long)items) return;
+  const unsigned sig = item / (unsigned)nband;
+  const BandScale b = bands[item - sig * (unsigned)nband];
+  const int tid = threadIdx.x, lane = tid & 63, c = tid >> 6;
+  const long r0 = (long)rg * fft::kT;
+  const unsigned m1 = (unsigned)N1 - 1, mx = (unsigned)(Nx >> 9) - 1;
+  const int tr = lane & 15, kq = lane >> 4;
+  const int t = tr & 7, im_row = tr >> 3, jo = kq >> 1, zc = kq & 1;
+  const double* xs = (const double*)(Xn + (long)sig * Nx + 64 * c + tr) + zc;
+  const double* ps = psi + b.psi_off + 64 * c + tr;
+  // blocks j0 + 2 jo (jo = 0, 1: two blocks of one parity per MFMA)
+  auto load = [&](int j0, double (&xv)[4], double (&pv)[4], double& av) {
+    const int j = j0 + 2 * jo;
+    const bool in = j < b.nb;
+    const int jj = in ? j : b.nb - 1;
+    const unsigned k1 = ((unsigned)b.b0 + jj) & m1, kx = ((unsigned)b.fb0 + jj) & mx;
+    const double4 w = wN1[(k1 * ((unsigned)r0 + t)) & m1];
+    av = im_row ? (zc ? w.x : w.y) : (zc ? -w.y : w.x);
+    av = in ? av : 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      xv[q] = xs[2 * (512L * kx + 16 * q)];
+      pv[q] = ps[512 * jj + 16 * q];
+    }
+  };
+  auto sums = [&](int par, d4v (&acc)[4]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = d4v{0.0, 0.0, 0.0, 0.0};
+    double xv[4], pv[4], av;
+    load(par, xv, pv, av);
+    for (int j0 = par; j0 < b.nb; j0 += 4) {
+#if JW_CWT_PAR_PF  // the next pair's loads before this pair's MFMAs (16 more VGPRs)
+      double xn[4], pn[4], an;
+      load(j0 + 4, xn, pn, an);
+#endif
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, xv[q] * pv[q], acc[q], 0, 0, 0);
+#if JW_CWT_PAR_PF
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        xv[q] = xn[q];
+        pv[q] = pn[q];
+      }
+      av = an;
+#else
+      load(j0 + 4, xv, pv, av);
+#endif
+    }
+  };
+  d4v lo[4], hi[4];
+  sums(0, lo);
+  sums(1, hi);
+  // j even <-> k1 parity of b0 (N1 is even): hi = +-(S_j-even - S_j-odd)
+  const double sg = (b.b0 & 1) ? -1.0 : 1.0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const d4v e = lo[q], o = hi[q];
+    lo[q] = e + o;
+    hi[q] = sg * (e - o);
+  }
+  const Out o = out.at(item, sig, b.s);
+  auto finish = [&](const d4v (&acc)[4], long rb) {
+    double im[8];
+    const int t0 = lane >> 4;
+    __syncthreads();  // the previous group's staging reads are done with the tile
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const long n1 = rb + t0 + 4 * e, col0 = 64 * c + tr;
+      cplx w0 = fft::twiddle(T, (n1 * col0) & (N - 1));
+      const cplx st = fft::twiddle(T, (16 * n1) & (N - 1));
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const cplx v = fft::cmul(make_double2(acc[q][e], acc[q][e + 2]), w0);
+        tile[(t0 + 4 * e) * 512 + (int)col0 + 16 * q] = v.x;
+        im[4 * e + q] = v.y;
+        if (q < 3) w0 = fft::cmul(w0, st);
+      }
+    }
+    cplx a[8];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) a[r].x = tile[c * 512 + lane + 64 * r];
+    __syncthreads();
+    const int col0 = 64 * c + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) tile[(t0 + 4 * (i >> 2)) * 512 + col0 + 16 * (i & 3)] = im[i];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) a[r].y = tile[c * 512 + lane + 64 * r];
+    __syncthreads();
+    fft::pass512_tail_split<1, false>(a, o, N, 512L, T, 0L, rb, tile);
+  };
+  finish(lo, r0);
+  // nothing of the second group's tail may be hoisted into the first's (its values would be live
+  // through the first tail: spills)
+  __builtin_amdgcn_sched_barrier(0);
+  finish(hi, r0 + N1 / 2);
+}
 
 // ---------------------------------------------------------------------------------------
 // Band scales on a coarse grid.  A scale whose band (signed bins lo .. hi, centred on the
@@ -1032,6 +1156,10 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   // the Kaiser-Bessel interpolation to the N-point coefficients, a few signals at a time so
   // that U stays ~128 MB
   if (!groups.empty() && st == JW_OK) {
+    // grids of 16+ rows: two row groups per workgroup from one set of band sums
+    // (cwt_band512_par); env JW_CWT_PAR=0 (A/B runs): one row group per workgroup
+    const char* gpr = std::getenv("JW_CWT_PAR");
+    const bool use_par = !(gpr && gpr[0] == '0');
     const bool nt = (ntm & 2) != 0;
     long woff = 0, roff = 0;
     for (size_t g = 0; g < groups.size() && st == JW_OK; ++g) {
@@ -1059,13 +1187,20 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
       for (long sg0 = 0; sg0 < batch; sg0 += gchunk[g]) {
         const long cs = std::min<long>(gchunk[g], batch - sg0);
         const long items = cs * G.n;
-        const long blocks = (items + 7) / 8 * 8 * (N1c / fft::kT);
+        const bool par = use_par && N1c >= 2 * fft::kT;
+        const long blocks = (items + 7) / 8 * 8 * (N1c / fft::kT / (par ? 2 : 1));
         const long iblocks = items * chunks;
         if (blocks > 0x7fffffffL || iblocks > 0x7fffffffL)
           return fail(JW_ERR_UNSUPPORTED, "CWT coarse grid too large");
-        hipLaunchKernelGGL((cwt_band512<true, true, 6, CoarseOut>), dim3((unsigned)blocks), dim3(512), 0,
-                           bs, Xn + sg0 * N, psi, gb, G.n, wN1c, M, N1c, items,
-                           CoarseOut{(double*)U, M, N1c, 0}, TM, 1, N);
+        if (par) {
+          hipLaunchKernelGGL(cwt_band512_par<CoarseOut>, dim3((unsigned)blocks), dim3(512), 0, bs,
+                             Xn + sg0 * N, psi, gb, G.n, wN1c, M, N1c, items,
+                             CoarseOut{(double*)U, M, N1c, 0}, TM, N);
+        } else {
+          hipLaunchKernelGGL((cwt_band512<true, true, 6, CoarseOut>), dim3((unsigned)blocks),
+                             dim3(512), 0, bs, Xn + sg0 * N, psi, gb, G.n, wN1c, M, N1c, items,
+                             CoarseOut{(double*)U, M, N1c, 0}, TM, 1, N);
+        }
         JW_HIP_TRY(hipGetLastError());
         auto interp = [&](auto lp) {
           constexpr int LP = decltype(lp)::value;
