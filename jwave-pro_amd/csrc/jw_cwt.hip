@@ -889,7 +889,7 @@ static void interp_weights(long P, long N, std::vector<double>& wt) {
 }
 
 // Group sizes: signals per forward chunk and (signal, scale) pairs per inverse group, so the
-// workspace A stays ~128 MB (Infinity Cache sized) at N = 2^18.
+// workspace A stays ~96 MB at N = 2^18 (two of them when pipelined).
 int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
                    const double* scales_host, int ns, double fs, int padding, double* out,
                    int batch, hipStream_t s) {
@@ -988,10 +988,15 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   }
   const int nband = (int)bands.size(), nfull = (int)full.size();
   const char* gmb = std::getenv("JW_CWT_GROUP_MB");  // A/B runs: workspace size in MiB
-  const long ws = (gmb ? std::atol(gmb) : 128L) << 20;
+  const long ws = (gmb ? std::atol(gmb) : 96L) << 20;  // 96 MB: profiles/r05/ab/cwt_group_p.txt
   const long per = std::max(1L, ws / (N * (long)sizeof(cplx)));
   const long pairs = (long)batch * nfull;  // two-pass pairs
-  const long gsig = std::min<long>(batch, per), gpair = std::max(1L, std::min<long>(pairs, per));
+  // two-pass groups of whole signals (all of a signal's two-pass scales in one group) when they
+  // fit the workspace: the group's pass 1 then reads one signal's spectrum, which stays cached
+  // (cfg3, 24 two-pass scales: 24-pair groups in a 96 MB workspace 27.7-27.9 ms against 32-pair
+  // groups in 128 MB 29.0-29.2 ms; 80 / 112 MB 29.1 / 28.5 ms; profiles/r05/ab/cwt_group_*.txt)
+  const long per_g = nfull > 0 && per >= nfull ? per / nfull * nfull : per;
+  const long gsig = std::min<long>(batch, per), gpair = std::max(1L, std::min<long>(pairs, per_g));
   // N = 2^18 (512 x 512): the pairs' inverse FFTs are software-pipelined over two workspaces
   // (run_fft512_pipelined); env JW_CWT_PIPE=0 runs the groups one after the other (A/B runs).
   const char* gpp = std::getenv("JW_CWT_PIPE");
