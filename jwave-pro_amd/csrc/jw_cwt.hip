@@ -696,26 +696,35 @@ __global__ __launch_bounds__(256) void cwt_interp_psi(const BandScale* bands, do
   psi[b.psi_off + e] = psi_bin<K>(w, scales, sc, b.s, k, N, fs).x / kb_phi_hat((double)(kk - b.kc) / (double)M);
 }
 
-// One workgroup = kInterpTC consecutive coefficients t of one (signal, scale) pair from its
-// coarse row U[item] (M = N / 2^LOGP samples).  The coarse samples the chunk needs are staged
-// in LDS; lane l of wave v takes t = t0 + v kInterpTC / 4 + l + 64 i, so its r = t mod P is fixed
-// (P <= 64) and its 17 weights phi(r / P + 8 - k) / N (wtab, host-made) stay in registers; the
-// lanes of one s0 = t / P read the same samples (LDS broadcast).  The phase e^{2 pi i kc t / N}
-// is one table lookup per lane, then a wave-uniform step per 64 outputs.
-constexpr int kInterpTC = 4096;
+// One workgroup = interp_tc<LOGP>() = 1024 P consecutive coefficients t of one (signal, scale)
+// pair from its coarse row U[item] (M = N / P samples, P = 2^LOGP): the 1024 + 17 coarse samples
+// the chunk needs are staged in LDS.  Lane l of wave v takes t = t0 + v TC / 4 + l + 64 i, so
+// its r = t mod P is fixed (P <= 64) and its 17 weights phi(r / P + 8 - k) / N (wtab, host-made)
+// stay in registers; the lanes of one s0 = t / P read the same samples (LDS broadcast).  The
+// phase e^{2 pi i kc t / N} is a table lookup per lane every 32 outputs and a wave-uniform step
+// per 64 positions in between.  (Chunks of 4096 for every P ran the P = 32, 64 grids at 5.3-5.4
+// TB/s against 6.2-6.3 for P = 4, 8: their per-workgroup start -- 17 weight loads per lane, the
+// staging, the phase lookups -- is amortised over P / 4 times more outputs now.)
+template <int LOGP>
+constexpr long interp_tc() {
+  return 1024L << LOGP;
+}
 template <int LOGP>
 __global__ __launch_bounds__(256) void cwt_interp(const cplx* __restrict__ U, long M,
                                                   const BandScale* __restrict__ bands, int nsc,
                                                   const double* __restrict__ wtab, long N, long n,
                                                   int ns, long sig0, double* __restrict__ out,
                                                   bool nt, Tables T, int chunks) {
-  constexpr int P = 1 << LOGP, NU = kInterpTC / P + kInterpTaps, PER = kInterpTC / 4 / 64;
+  constexpr int P = 1 << LOGP;
+  constexpr long TC = interp_tc<LOGP>();
+  constexpr int NU = (int)(TC / P) + kInterpTaps, PER = (int)(TC / 4 / 64), RS = 32;
+  static_assert(PER % RS == 0 || PER < RS, "phase resync period");
   __shared__ cplx us[NU];
   const unsigned bid = blockIdx.x, item = bid / (unsigned)chunks;
   const unsigned chunk = bid - item * (unsigned)chunks;
   const unsigned sl = item / (unsigned)nsc;
   const BandScale b = bands[item - sl * (unsigned)nsc];
-  const long t0 = (long)chunk * kInterpTC;
+  const long t0 = (long)chunk * TC;
   const cplx* u = U + (long)item * M;
   const long s_lo = (t0 >> LOGP) - kInterpHalf;  // first staged sample (mod M)
   for (int j = threadIdx.x; j < NU; j += 256) {
@@ -724,38 +733,40 @@ __global__ __launch_bounds__(256) void cwt_interp(const cplx* __restrict__ U, lo
     us[j] = u[q];
   }
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const long tl = t0 + (long)wv * (kInterpTC / 4) + lane;  // this lane's first output
+  const long tl = t0 + (long)wv * (TC / 4) + lane;  // this lane's first output
   const int r = (int)(tl & (P - 1));
   double wr[kInterpTaps];
 #pragma unroll
   for (int k = 0; k < kInterpTaps; ++k) wr[k] = wtab[r * kInterpStride + k];
   const long kcu = ((b.kc % N) + N) % N;
-  cplx ph = fft::twiddle(T, (kcu * tl) & (N - 1));
   const cplx st = fft::twiddle(T, (kcu * 64) & (N - 1));
   double* row = out + 2 * ((sig0 + sl) * ns + b.s) * n;
   __syncthreads();
   const int base0 = (int)((tl >> LOGP) - (t0 >> LOGP));
+  for (int i0 = 0; i0 < PER; i0 += RS) {
+    cplx ph = fft::twiddle(T, (kcu * (tl + 64L * i0)) & (N - 1));
 #pragma unroll 4
-  for (int i = 0; i < PER; ++i) {
-    const long t = tl + 64 * i;
-    const int base = base0 + ((64 * i) >> LOGP);
-    double ar = 0.0, ai = 0.0;
+    for (int i = i0; i < i0 + (PER < RS ? PER : RS); ++i) {
+      const long t = tl + 64 * i;
+      const int base = base0 + ((64 * i) >> LOGP);
+      double ar = 0.0, ai = 0.0;
 #pragma unroll
-    for (int k = 0; k < kInterpTaps; ++k) {
-      const cplx v = us[base + k];
-      ar = __builtin_fma(wr[k], v.x, ar);
-      ai = __builtin_fma(wr[k], v.y, ai);
-    }
-    const cplx y = fft::cmul(make_double2(ar, ai), ph);
-    if (t < n) {
-      cplx* o = (cplx*)(row + 2 * t);
-      if (nt) {
-        fft::nt_store(o, y);
-      } else {
-        *o = y;
+      for (int k = 0; k < kInterpTaps; ++k) {
+        const cplx v = us[base + k];
+        ar = __builtin_fma(wr[k], v.x, ar);
+        ai = __builtin_fma(wr[k], v.y, ai);
       }
+      const cplx y = fft::cmul(make_double2(ar, ai), ph);
+      if (t < n) {
+        cplx* o = (cplx*)(row + 2 * t);
+        if (nt) {
+          fft::nt_store(o, y);
+        } else {
+          *o = y;
+        }
+      }
+      ph = fft::cmul(ph, st);
     }
-    ph = fft::cmul(ph, st);
   }
 }
 
@@ -1188,14 +1199,13 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
       const double* gw = dwt + woff;
       woff += P * kInterpStride;
       roff += N1c;
-      const int chunks = (int)((n + kInterpTC - 1) / kInterpTC);
+
       for (long sg0 = 0; sg0 < batch; sg0 += gchunk[g]) {
         const long cs = std::min<long>(gchunk[g], batch - sg0);
         const long items = cs * G.n;
         const bool par = use_par && N1c >= 2 * fft::kT;
         const long blocks = (items + 7) / 8 * 8 * (N1c / fft::kT / (par ? 2 : 1));
-        const long iblocks = items * chunks;
-        if (blocks > 0x7fffffffL || iblocks > 0x7fffffffL)
+        if (blocks > 0x7fffffffL)
           return fail(JW_ERR_UNSUPPORTED, "CWT coarse grid too large");
         if (par) {
           hipLaunchKernelGGL(cwt_band512_par<CoarseOut>, dim3((unsigned)blocks), dim3(512), 0, bs,
@@ -1207,20 +1217,24 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
                              CoarseOut{(double*)U, M, N1c, 0}, TM, 1, N);
         }
         JW_HIP_TRY(hipGetLastError());
-        auto interp = [&](auto lp) {
+        auto interp = [&](auto lp) -> int {
           constexpr int LP = decltype(lp)::value;
+          constexpr long TC = interp_tc<LP>();
+          const long chunks = (n + TC - 1) / TC, iblocks = items * chunks;
+          if (iblocks > 0x7fffffffL) return fail(JW_ERR_UNSUPPORTED, "CWT coarse grid too large");
           hipLaunchKernelGGL(cwt_interp<LP>, dim3((unsigned)iblocks), dim3(256), 0, bs, U, M, gb,
-                             G.n, gw, N, n, ns, sg0, out, nt, T, chunks);
+                             G.n, gw, N, n, ns, sg0, out, nt, T, (int)chunks);
+          return JW_OK;
         };
         switch (P) {
-          case 1: interp(std::integral_constant<int, 0>{}); break;
-          case 2: interp(std::integral_constant<int, 1>{}); break;
-          case 4: interp(std::integral_constant<int, 2>{}); break;
-          case 8: interp(std::integral_constant<int, 3>{}); break;
-          case 16: interp(std::integral_constant<int, 4>{}); break;
-          case 32: interp(std::integral_constant<int, 5>{}); break;
-          default: interp(std::integral_constant<int, 6>{}); break;
+          case 2: st = interp(std::integral_constant<int, 1>{}); break;
+          case 4: st = interp(std::integral_constant<int, 2>{}); break;
+          case 8: st = interp(std::integral_constant<int, 3>{}); break;
+          case 16: st = interp(std::integral_constant<int, 4>{}); break;
+          case 32: st = interp(std::integral_constant<int, 5>{}); break;
+          default: st = interp(std::integral_constant<int, 6>{}); break;
         }
+        if (st != JW_OK) return st;
         JW_HIP_TRY(hipGetLastError());
       }
     }
