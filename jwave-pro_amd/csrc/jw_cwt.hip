@@ -659,19 +659,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
 // and f is interpolated from the coarse samples u[s] = sum_m (Z[kc + m] / Phi(m / M)) e^{2 pi i m s / M}
 // (an M-point inverse DFT, run by the band kernel on the coarse grid) with a Kaiser-Bessel kernel
 // phi of width W: f(tau) = sum_s u[s] phi(tau - s) up to the kernel's aliasing, Phi being phi's
-// Fourier transform (the deconvolution; Jackson et al. 1991).  Oversampling M >= 3 |m|max
-// (sigma = 1.5) with W = 16 bounds that error near 1e-14 of the scale's peak (numpy prototype
-// over the cfg3 scales: <= 1.7e-14; tests/test_cwt_gpu.py).  The coarse transform is P times
+// Fourier transform (the deconvolution; Jackson et al. 1991).  Oversampling M >= 2.5 |m|max
+// (sigma = 1.25) with W = 18 bounds that error near 1e-14 of the scale's peak (numpy prototype
+// over the cfg3 scales: <= 1.2e-14; tests/test_cwt_gpu.py).  The coarse transform is P times
 // smaller than the scale's N-point one; the interpolation reads it from L2 and writes each
 // coefficient once, in 1 KB pieces per wave.
 // ---------------------------------------------------------------------------------------
-constexpr int kInterpW = 16;                   // kernel width (coarse samples)
+constexpr int kInterpW = 18;                   // kernel width (coarse samples)
 constexpr int kInterpHalf = kInterpW / 2;
-constexpr int kInterpTaps = 2 * kInterpHalf + 1;  // taps per output: s0 - 8 .. s0 + 8
+constexpr int kInterpTaps = 2 * kInterpHalf + 1;  // taps per output: s0 - 9 .. s0 + 9
 constexpr int kInterpStride = 20;              // weights per r in the table
-constexpr double kInterpSigma = 1.5;           // minimum oversampling of the band on the grid
+constexpr double kInterpSigma = 1.25;           // minimum oversampling of the band on the grid
 // beta = pi sqrt((W / sigma)^2 (sigma - 1/2)^2 - 0.8) (Beatty et al. 2005)
-constexpr double kInterpBeta = 33.39230409511825;
+constexpr double kInterpBeta = 33.812645176356604;
 
 // Phi(nu) = W sinh(sqrt(beta^2 - (pi W nu)^2)) / sqrt(...), the transform of
 // phi(x) = I0(beta sqrt(1 - (2x/W)^2)), |x| <= W/2 (|nu| <= 1/2 here, so the root is real)
@@ -697,9 +697,9 @@ __global__ __launch_bounds__(256) void cwt_interp_psi(const BandScale* bands, do
 }
 
 // One workgroup = interp_tc<LOGP>() = 1024 P consecutive coefficients t of one (signal, scale)
-// pair from its coarse row U[item] (M = N / P samples, P = 2^LOGP): the 1024 + 17 coarse samples
+// pair from its coarse row U[item] (M = N / P samples, P = 2^LOGP): the 1024 + 19 coarse samples
 // the chunk needs are staged in LDS.  Lane l of wave v takes t = t0 + v TC / 4 + l + 64 i, so
-// its r = t mod P is fixed (P <= 64) and its 17 weights phi(r / P + 8 - k) / N (wtab, host-made)
+// its r = t mod P is fixed (P <= 64) and its 19 weights phi(r / P + 9 - k) / N (wtab, host-made)
 // stay in registers; the lanes of one s0 = t / P read the same samples (LDS broadcast).  The
 // phase e^{2 pi i kc t / N} is a table lookup per lane every 32 outputs and a wave-uniform step
 // per 64 positions in between.  (Chunks of 4096 for every P ran the P = 32, 64 grids at 5.3-5.4

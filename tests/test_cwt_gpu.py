@@ -162,9 +162,9 @@ def test_band_scales_one_pass(kind, n, monkeypatch):
 def test_coarse_grid_scales(kind, n, pmin, monkeypatch):
     # Band scales whose band fits a grid of M = N / P points (P >= JW_CWT_INTERP) run as an
     # M-point inverse DFT (the band kernel on the coarse grid, the band divided by the
-    # Kaiser-Bessel kernel's transform) and a 17-tap interpolation to the N-point coefficients.
+    # Kaiser-Bessel kernel's transform) and a 19-tap interpolation to the N-point coefficients.
     # Against the same scales through the two-pass FFT (JW_CWT_INTERP=0, JW_CWT_BAND=0): the
-    # interpolation error is ~1e-14 of each scale's peak (W = 16, oversampling 1.5); against the
+    # interpolation error is ~1e-14 of each scale's peak (W = 18, oversampling 1.25); against the
     # oracle per scale as the other paths.  pmin = 2 also runs the P = 2 grids.
     scales = CWT.generateLogScales(2.0, 1024.0, 14)
     wv, params = {"morlet": (MorletWavelet(*MORLET6), MORLET6),
