@@ -184,6 +184,27 @@ def test_coarse_grid_scales(kind, n, pmin, monkeypatch):
             assert nw(got[i], ex[i]) < 1e-11, (i, nw(got[i], ex[i]))
 
 
+def test_coarse_grid_workspace_chunks(monkeypatch):
+    # The coarse rows of a group go through a ~128 MB workspace a few signals at a time: at
+    # N = 2^18 the P = 4 grids (65536 points) hold 17 signals of 7 scales, so 20 signals take
+    # two chunks.  Same values as the two-pass FFT per scale, and the same bits whether the
+    # signals come in one call or one at a time (the chunking changes no operation).
+    import torch
+    n = 1 << 18
+    scales = np.array([17.7, 19.5, 21.5, 23.8, 26.3, 29.0, 32.0])
+    xs = np.stack([orc.fill_uniform(n, 60 + b) for b in range(20)])
+    t = CWT(MorletWavelet(*MORLET6))
+    got = t.transformFFTBatch(torch.from_numpy(xs).cuda(), scales, 1.0).cpu().numpy()
+    one = t.transformFFT(xs[19], scales, 1.0).getCoefficients()
+    assert np.array_equal(got[19], one)
+    monkeypatch.setenv("JW_CWT_INTERP", "0")
+    monkeypatch.setenv("JW_CWT_BAND", "0")
+    for b in (0, 16, 19):
+        two = t.transformFFT(xs[b], scales, 1.0).getCoefficients()
+        for i in range(len(scales)):
+            assert nw(got[b, i], two[i]) < 1e-12, (b, i, nw(got[b, i], two[i]))
+
+
 @pytest.mark.parametrize("kind", ["morlet", "mexhat"])
 def test_band_and_pass1_variants_bit_identical(kind, monkeypatch):
     # The band kernel's schedules (JW_CWT_BAND_V: load prefetch, one or eight row groups per
