@@ -1083,9 +1083,19 @@ __global__ __launch_bounds__(kTailNT) void fwt_cols_tail(const double* in, doubl
   const int line0 = (int)(blockIdx.x % nchunk) * kTailNL;
   const double* src = in + mat * ms_in + line0;
   double* dst = out + mat * ms_out + line0;
-  for (int k = tid; k < len * kTailNL; k += kTailNT) {
-    const int i = k / kTailNL, c = k % kTailNL;
-    bufs[c * PAD + i] = src[(long)i * cols + c];
+  // every load issued before the first LDS write (a load-then-store loop waited out one HBM
+  // latency per row piece: fwt_cols_tail ran at 1.7-3.0 TB/s)
+  constexpr int KL = kTailLen * kTailNL / kTailNT;
+  double v[KL];
+#pragma unroll
+  for (int q = 0; q < KL; ++q) {
+    const int k = tid + q * kTailNT, i = k / kTailNL, c = k % kTailNL;
+    v[q] = i < len ? src[(long)i * cols + c] : 0.0;
+  }
+#pragma unroll
+  for (int q = 0; q < KL; ++q) {
+    const int k = tid + q * kTailNT, i = k / kTailNL, c = k % kTailNL;
+    if (i < len) bufs[c * PAD + i] = v[q];
   }
   __syncthreads();
   double* buf = bufs + g * PAD;
@@ -1099,9 +1109,15 @@ __global__ __launch_bounds__(kTailNT) void fwt_cols_tail(const double* in, doubl
     cascade_fwd<FMA, M, NTL, kTailLen, WS>(buf, len, lvl_h0, tw, lt, f);
   }
   if (WS) __syncthreads();  // the stores below read other waves' columns
-  for (int k = tid; k < len * kTailNL; k += kTailNT) {
-    const int i = k / kTailNL, c = k % kTailNL;
-    dst[(long)i * cols + c] = bufs[c * PAD + i];
+#pragma unroll
+  for (int q = 0; q < KL; ++q) {
+    const int k = tid + q * kTailNT, i = k / kTailNL, c = k % kTailNL;
+    v[q] = i < len ? bufs[c * PAD + i] : 0.0;
+  }
+#pragma unroll
+  for (int q = 0; q < KL; ++q) {
+    const int k = tid + q * kTailNT, i = k / kTailNL, c = k % kTailNL;
+    if (i < len) dst[(long)i * cols + c] = v[q];
   }
 }
 
