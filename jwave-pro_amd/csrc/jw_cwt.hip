@@ -696,18 +696,22 @@ __global__ __launch_bounds__(256) void cwt_interp_psi(const BandScale* bands, do
   psi[b.psi_off + e] = psi_bin<K>(w, scales, sc, b.s, k, N, fs).x / kb_phi_hat((double)(kk - b.kc) / (double)M);
 }
 
-// One workgroup = interp_tc<LOGP>() = 1024 P consecutive coefficients t of one (signal, scale)
+// One workgroup = interp_tc<LOGP>() = min(1024 P, 8192) consecutive coefficients t of one (signal, scale)
 // pair from its coarse row U[item] (M = N / P samples, P = 2^LOGP): the 1024 + 19 coarse samples
 // the chunk needs are staged in LDS.  Lane l of wave v takes t = t0 + v TC / 4 + l + 64 i, so
 // its r = t mod P is fixed (P <= 64) and its 19 weights phi(r / P + 9 - k) / N (wtab, host-made)
 // stay in registers; the lanes of one s0 = t / P read the same samples (LDS broadcast).  The
 // phase e^{2 pi i kc t / N} is a table lookup per lane every 32 outputs and a wave-uniform step
 // per 64 positions in between.  (Chunks of 4096 for every P ran the P = 32, 64 grids at 5.3-5.4
-// TB/s against 6.2-6.3 for P = 4, 8: their per-workgroup start -- 17 weight loads per lane, the
-// staging, the phase lookups -- is amortised over P / 4 times more outputs now.)
+// TB/s against 6.2-6.3 for P = 4, 8; 65536 for P = 64 took it 1116 -> 1062 us, 8192 -> 1000 us:
+// the per-workgroup start -- the weight loads, the staging, the phase lookups -- amortised over
+// more outputs, with enough workgroups left for an even finish; profiles/r05/ab/cwt_interp_tc_z.txt)
+#ifndef JW_INTERP_TCMAX  // A/B builds: the largest chunk
+#define JW_INTERP_TCMAX 8192
+#endif
 template <int LOGP>
 constexpr long interp_tc() {
-  return 1024L << LOGP;
+  return (1024L << LOGP) < JW_INTERP_TCMAX ? (1024L << LOGP) : JW_INTERP_TCMAX;
 }
 template <int LOGP>
 __global__ __launch_bounds__(256) void cwt_interp(const cplx* __restrict__ U, long M,
