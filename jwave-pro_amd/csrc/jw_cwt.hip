@@ -911,7 +911,8 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   if (n == 0 || ns == 0 || batch == 0) return JW_OK;
   long N = 1;
   while (N < n) N <<= 1;  // MathUtils.nextPowerOfTwo :46-49
-  if (N > (1L << 24)) return fail(JW_ERR_UNSUPPORTED, "CWT padded length %ld > 2^24", N);
+  // 2^25 and 2^26 run the generic four-step passes (8192-point lines in 128 KB of LDS)
+  if (N > (1L << 26)) return fail(JW_ERR_UNSUPPORTED, "CWT padded length %ld > 2^26", N);
   if ((long)batch * ns >= (1L << 31))
     return fail(JW_ERR_UNSUPPORTED, "CWT batch x scales = %ld >= 2^31", (long)batch * ns);
   Tables T;

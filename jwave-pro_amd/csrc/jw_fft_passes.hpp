@@ -477,6 +477,14 @@ int run_fft(long N, long items, In1 in1, Out1 out_single, Out2 out_final, cplx* 
   }
   const int log1 = (logN + 1) / 2, log2 = logN - log1;
   const long N1 = 1L << log1, N2 = 1L << log2;
+  if (N1 > 8192) return fail(JW_ERR_UNSUPPORTED, "FFT length %ld > 2^26", N);
+  // lines of 8192 points (N = 2^25, 2^26) stage 128 KB of LDS: past the 64 KB default
+  auto lds_ok = [](auto kern, long M) -> hipError_t {
+    const size_t b = (size_t)M * sizeof(cplx);
+    return b > 65536 ? hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)b)
+                     : hipSuccess;
+  };
   ColOut a_out{A, N, N2, a_nt};
   RowIn a_in{A, N, N2};
   if (N1 == 512) {
@@ -484,6 +492,7 @@ int run_fft(long N, long items, In1 in1, Out1 out_single, Out2 out_final, cplx* 
                        dim3((unsigned)(N2 / kT), (unsigned)items), dim3(512), 0, s, in1, a_out, N,
                        N2, T);
   } else {
+    JW_HIP_TRY(lds_ok(pass_generic<S, true, In1, ColOut>, N1));
     hipLaunchKernelGGL((pass_generic<S, true, In1, ColOut>), dim3((unsigned)N2, (unsigned)items),
                        dim3(256), (size_t)N1 * sizeof(cplx), s, in1, a_out, N, N2, log1, T);
   }
@@ -493,6 +502,7 @@ int run_fft(long N, long items, In1 in1, Out1 out_single, Out2 out_final, cplx* 
                        dim3((unsigned)(N1 / kT), (unsigned)items), dim3(512), 0, s, a_in, out_final,
                        N, N2, T);
   } else {
+    JW_HIP_TRY(lds_ok(pass_generic<S, false, RowIn, Out2>, N2));
     hipLaunchKernelGGL((pass_generic<S, false, RowIn, Out2>), dim3((unsigned)N1, (unsigned)items),
                        dim3(256), (size_t)N2 * sizeof(cplx), s, a_in, out_final, N, N2, log2, T);
   }

@@ -270,14 +270,22 @@ static void fft_ct(double* x, long n, int inverse, int normalize) {
     double wr, wi;
     java_sincos(angle, &wi, &wr);
     long half = size / 2;
+    double* tw = NULL; /* exact twiddles of this size, computed once (not per block) */
+    if (g_exact_twiddles) {
+      tw = (double*)malloc(sizeof(double) * 2 * half);
+      for (long k = 0; k < half; k++) {
+        const long double a = (long double)2 * 3.141592653589793238462643383279503L *
+                              (long double)k / (long double)size * (inverse ? 1 : -1);
+        tw[2 * k] = (double)cosl(a);
+        tw[2 * k + 1] = (double)sinl(a);
+      }
+    }
     for (long start = 0; start < n; start += size) {
       double nr = 1, ni = 0; /* wn = (1,0) */
       for (long k = 0; k < half; k++) {
-        if (g_exact_twiddles) {
-          const long double a = (long double)2 * 3.141592653589793238462643383279503L *
-                                (long double)k / (long double)size * (inverse ? 1 : -1);
-          nr = (double)cosl(a);
-          ni = (double)sinl(a);
+        if (tw) {
+          nr = tw[2 * k];
+          ni = tw[2 * k + 1];
         }
         double* u = x + 2 * (start + k);
         double* v = x + 2 * (start + k + half);
@@ -291,6 +299,7 @@ static void fft_ct(double* x, long n, int inverse, int normalize) {
         nr = nnr; ni = nni;
       }
     }
+    free(tw);
   }
   if (inverse && normalize) { /* :207-211  x[i].mul(1.0/n) */
     double s = 1.0 / (double)n;

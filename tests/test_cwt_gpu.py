@@ -84,6 +84,47 @@ def test_four_step_lengths(n):
     check(MorletWavelet(*MORLET6), "morlet", MORLET6, n, scales, PaddingType.SYMMETRIC, fs=2.5)
 
 
+def np_cwt_morlet(x, scales, fs, params):
+    """transformFFT for Morlet with zero padding, restated on numpy's FFT (correctly rounded
+    twiddles, error ~1e-16 log N): omega and psi_hat as the oracle's jwo_cwt_fft /
+    jwo_cwt_wavelet_ft_c (ContinuousWaveletTransform.java, MorletWavelet.java:117-125)."""
+    n = x.shape[0]
+    N = 1 << max(0, (n - 1).bit_length())
+    X = np.fft.fft(np.concatenate([x, np.zeros(N - n)]))
+    om = 2.0 * math.pi * np.arange(N) * fs / N
+    om[N // 2 + 1:] -= 2.0 * math.pi * fs
+    fb, fc = params
+    out = np.empty((len(scales), n), complex)
+    for i, a in enumerate(scales):
+        f = a * om / (2.0 * math.pi)
+        psi = math.sqrt(2.0 * math.pi * fb) * np.exp(-2.0 * math.pi ** 2 * fb * (f - fc) ** 2)
+        out[i] = np.fft.ifft(X * (psi * math.sqrt(a)))[:n]
+    return out
+
+
+@pytest.mark.parametrize("n", [(1 << 24) + 5, (1 << 25) + 1])
+def test_lengths_past_2_24(n):
+    # nextPowerOfTwo(n) = 2^25, 2^26 (JWave pads with no cap): 8192-point lines through the
+    # generic passes in 128 KB of LDS; scale 2 runs two-pass, 900 on a coarse grid.  Checked
+    # per scale against the numpy restatement, which at 2^25 is itself checked against the
+    # oracle with exact twiddles (~50 s of CPU; at 2^26 the oracle would take ~2 minutes).
+    scales = np.array([2.0, 900.0])
+    x = orc.fill_uniform(n, 7)
+    got = CWT(MorletWavelet(*MORLET6), PaddingType.ZERO).transformFFT(x, scales, 1.0).getCoefficients()
+    ref = np_cwt_morlet(x, scales, 1.0, MORLET6)
+    for i in range(len(scales)):
+        assert nw(got[i], ref[i]) < TOL_EXACT, (i, nw(got[i], ref[i]))
+    if n < (1 << 25):
+        ex = orc.cwt_fft(x, scales, 1.0, "morlet", MORLET6, 0, exact=True)
+        assert nw(ref, ex) < TOL_EXACT
+        assert nw(got, ex) < TOL_EXACT
+
+
+def test_length_past_2_26_refused():
+    with pytest.raises(NotImplementedError, match="2\\^26"):
+        CWT(MorletWavelet(*MORLET6)).transformFFT(np.zeros((1 << 26) + 1), np.array([4.0]), 1.0)
+
+
 def test_batch_and_device_tensors(device):
     import torch
     n, B = 1 << 18, 3
