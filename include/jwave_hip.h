@@ -83,6 +83,15 @@ int jw_get_device(int* ordinal);
  * in flight (and the kernels they queued) before freeing; later calls rebuild what they need.
  * Returns the bytes of tables freed (>= 0). */
 long jw_release_caches(void);
+/* Engine settings for same-box A/B runs and tests (not part of the reference interface): the
+ * JW_* names the engine consults (JW_CWT_INTERP, JW_FWT_GENERIC, JW_INV_KERNEL, ...; DESIGN.md
+ * §9).  Each is read from the environment once, on first use; jw_set_knob(name, value)
+ * replaces that value for later calls (value NULL = unset), so a test changes a setting without
+ * setenv racing the engine's threads.  name must start with "JW_" (else
+ * JW_ERR_ILLEGAL_ARGUMENT).  jw_get_knob returns the value in effect, or NULL when unset; the
+ * string stays valid for the life of the process. */
+int jw_set_knob(const char* name, const char* value);
+const char* jw_get_knob(const char* name);
 
 /* ======================================================================
  * MODWT  (replaces MODWTTransform.forwardMODWT :256 / inverseMODWT :337)

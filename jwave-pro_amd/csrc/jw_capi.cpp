@@ -74,6 +74,25 @@ std::shared_mutex& api_mutex() {
   return m;
 }
 
+namespace {
+std::mutex g_knob_mu;
+std::map<std::string, const std::string*>& knobs() {  // values are never freed: callers keep them
+  static std::map<std::string, const std::string*> m;
+  return m;
+}
+}  // namespace
+
+const char* knob(const char* name) {
+  std::lock_guard<std::mutex> lk(g_knob_mu);
+  auto& m = knobs();
+  auto it = m.find(name);
+  if (it == m.end()) {
+    const char* e = std::getenv(name);
+    it = m.emplace(name, e ? new std::string(e) : nullptr).first;
+  }
+  return it->second ? it->second->c_str() : nullptr;
+}
+
 void note_device_used(int dev) {
   if (dev >= 0 && dev < 64) g_used_devices.fetch_or(1ULL << dev, std::memory_order_relaxed);
 }
@@ -166,7 +185,7 @@ class CopyPool {
   };
   CopyPool() {
     int t = 0;
-    if (const char* e = std::getenv("JW_COPY_THREADS")) {
+    if (const char* e = knob("JW_COPY_THREADS")) {
       workers_ = std::max(0, std::atoi(e) - 1);
     } else {
       if (const char* o = std::getenv("OMP_NUM_THREADS")) t = std::atoi(o);
@@ -211,7 +230,7 @@ class CopyPool {
 // doubles per bounce buffer: 32 MiB (JW_PIN_MB for A/B runs)
 size_t pin_doubles() {
   static const size_t v = [] {
-    const char* e = std::getenv("JW_PIN_MB");
+    const char* e = knob("JW_PIN_MB");
     const long mb = e ? std::atol(e) : 32;
     return (size_t)std::max(1L, mb) << 17;
   }();
@@ -222,7 +241,7 @@ size_t pin_doubles() {
 constexpr int kMaxRing = 4;
 int pin_ring() {
   static const int v = [] {
-    const char* e = std::getenv("JW_PIN_RING");
+    const char* e = knob("JW_PIN_RING");
     const int r = e ? std::atoi(e) : 3;
     return std::max(2, std::min(kMaxRing, r));
   }();
@@ -505,6 +524,21 @@ long jw_release_caches(void) {
   const size_t freed = release_all_caches();
   trim_pools();
   return (long)freed;
+}
+
+int jw_set_knob(const char* name, const char* value) {
+  clear_error();
+  if (!name || std::strncmp(name, "JW_", 3) != 0)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "setting name must start with JW_");
+  (void)knob(name);  // the environment's value first, so it is not read later over this one
+  std::lock_guard<std::mutex> lk(g_knob_mu);
+  knobs()[name] = value ? new std::string(value) : nullptr;  // the old value stays allocated
+  return JW_OK;
+}
+
+const char* jw_get_knob(const char* name) {
+  clear_error();
+  return name ? knob(name) : nullptr;
 }
 
 // ---------------------------------------------------------------- MODWT

@@ -942,7 +942,7 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   } else {
     w.norm = std::sqrt(2.0 * kPi);  // MeyerWavelet.java:244
   }
-  const char* gnt = std::getenv("JW_CWT_NT");  // A/B runs: bit 1 = NT stores of A, 2 = of coeffs
+  const char* gnt = knob("JW_CWT_NT");  // A/B runs: bit 1 = NT stores of A, 2 = of coeffs
   const int ntm = gnt ? std::atoi(gnt) : 2;  // measured best: NT coefficient stores only
   w.p2 = wavelet == JW_CWT_MORLET ? -2.0 * kPi * kPi * w.p0 : -0.5 * w.p0 * w.p0;
   // Scales whose band spans at most nbmax 512-bin blocks run in one pass (cwt_band512); the
@@ -951,9 +951,9 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   // (profiles/r02/cwt_band_sweep_r02.log).  env JW_CWT_BAND (A/B runs): nbmax, 0 = all two-pass.
   // Before either, a band scale whose band fits a coarse grid of M = N / P points with P >=
   // pmin runs there (cwt_interp): env JW_CWT_INTERP (A/B runs and tests) = pmin, 0 = never.
-  const char* gbd = std::getenv("JW_CWT_BAND");
+  const char* gbd = knob("JW_CWT_BAND");
   const int nbmax = gbd ? std::atoi(gbd) : 32;
-  const char* gip = std::getenv("JW_CWT_INTERP");
+  const char* gip = knob("JW_CWT_INTERP");
   const long pmin = gip ? std::atol(gip) : 4;
   const long N1b = N / 512;
   std::vector<BandScale> bands, coarse;  // coarse: sorted by M below
@@ -1003,7 +1003,7 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     coarse = std::move(sorted);
   }
   const int nband = (int)bands.size(), nfull = (int)full.size();
-  const char* gmb = std::getenv("JW_CWT_GROUP_MB");  // A/B runs: workspace size in MiB
+  const char* gmb = knob("JW_CWT_GROUP_MB");  // A/B runs: workspace size in MiB
   const long ws = (gmb ? std::atol(gmb) : 96L) << 20;  // 96 MB: profiles/r05/ab/cwt_group_p.txt
   const long per = std::max(1L, ws / (N * (long)sizeof(cplx)));
   const long pairs = (long)batch * nfull;  // two-pass pairs
@@ -1015,8 +1015,8 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   const long gsig = std::min<long>(batch, per), gpair = std::max(1L, std::min<long>(pairs, per_g));
   // N = 2^18 (512 x 512): the pairs' inverse FFTs are software-pipelined over two workspaces
   // (run_fft512_pipelined); env JW_CWT_PIPE=0 runs the groups one after the other (A/B runs).
-  const char* gpp = std::getenv("JW_CWT_PIPE");
-  const char* gel = std::getenv("JW_CWT_EARLY");
+  const char* gpp = knob("JW_CWT_PIPE");
+  const char* gel = knob("JW_CWT_EARLY");
   const bool early = !(gel && gel[0] == '0');
   const bool pipe = N == (1L << 18) && pairs > gpair && !(gpp && gpp[0] == '0');
   StreamAllocs mem(s);
@@ -1114,7 +1114,7 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   // side cfg3 ran 32.0 ms against 30.6 one after the other (profiles/r05/ab/cwt_env_h.txt).
   // env JW_CWT_OVERLAP (A/B runs): 0 = never, 1 = whenever there are pairs.
   hipStream_t bs = s;
-  const char* gov = std::getenv("JW_CWT_OVERLAP");
+  const char* gov = knob("JW_CWT_OVERLAP");
   const bool overlap = gov ? gov[0] != '0' : nband > 0;
   if (st == JW_OK && (nband > 0 || !coarse.empty()) && pairs > 0) {
     if (overlap) {
@@ -1146,16 +1146,16 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     // A/B runs: JW_CWT_BAND_V = 2 x (three workgroups per CU, one row group each, instead of
     // two with R) + (load prefetch); JW_CWT_BAND_MFMA=0: VALU band sums.  Measured at cfg3
     // (profiles/r03/cwt_band_v.log): band kernel 15.5 (0) / 15.2 (1) / 14.4 (2) / 14.0 ms (3).
-    const char* gbv = std::getenv("JW_CWT_BAND_V");
+    const char* gbv = knob("JW_CWT_BAND_V");
     const int bv = gbv ? std::atoi(gbv) : 3;
-    const char* grr = std::getenv("JW_CWT_BAND_R");  // A/B runs: row groups per workgroup
+    const char* grr = knob("JW_CWT_BAND_R");  // A/B runs: row groups per workgroup
     int R = grr ? std::atoi(grr) : 8;  // two workgroups per CU: 1 -> 44.6, 8 -> 41.7 ms (r02)
     if (bv >= 2) R = 1;
     while (R > 1 && (N1b / fft::kT) % R) R >>= 1;
     R = std::max(1, std::min<int>(R, (int)(N1b / fft::kT)));
     const long blocks = (items + 7) / 8 * 8 * (N1b / fft::kT / R);
     if (blocks > 0x7fffffffL) return fail(JW_ERR_UNSUPPORTED, "CWT band grid too large");
-    const char* gmf = std::getenv("JW_CWT_BAND_MFMA");
+    const char* gmf = knob("JW_CWT_BAND_MFMA");
     auto band = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(512), 0, bs, Xn, psi, dbands, nband,
                          wN1, N, N1b, items, ob, T, R, N);
@@ -1179,7 +1179,7 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   if (!groups.empty() && st == JW_OK) {
     // grids of 16+ rows: two row groups per workgroup from one set of band sums
     // (cwt_band512_par); env JW_CWT_PAR=0 (A/B runs): one row group per workgroup
-    const char* gpr = std::getenv("JW_CWT_PAR");
+    const char* gpr = knob("JW_CWT_PAR");
     const bool use_par = !(gpr && gpr[0] == '0');
     const bool nt = (ntm & 2) != 0;
     long woff = 0, roff = 0;

@@ -1175,7 +1175,7 @@ __global__ __launch_bounds__(kNT) void transpose_kernel(const double* __restrict
 // 4096-sample rows use fwt_fwd_row / fwt_rev_row; env JW_FWT_ROW=0 keeps the runtime-level
 // cascades (A/B runs, tests).
 bool row_kernels() {
-  const char* e = std::getenv("JW_FWT_ROW");
+  const char* e = knob("JW_FWT_ROW");
   return !(e && e[0] == '0');
 }
 
@@ -1267,7 +1267,7 @@ bool launch_cols_nl(int M, int kind, bool rev, hipStream_t s, const double* in, 
 template <bool FMA>
 bool launch_cols(int M, int kind, bool rev, hipStream_t s, const double* in, double* out, int rows,
                  int cols, int lvl_h0, int tw, int batch, const Filters& f) {
-  const char* e = std::getenv("JW_FWT_LINES");
+  const char* e = knob("JW_FWT_LINES");
   if (e ? e[0] == '2' : rev)
     return launch_cols_nl<FMA, 2>(M, kind, rev, s, in, out, rows, cols, lvl_h0, tw, batch, f);
   return launch_cols_nl<FMA, 4>(M, kind, rev, s, in, out, rows, cols, lvl_h0, tw, batch, f);
@@ -1345,7 +1345,7 @@ int forward_t(const FwtPlan& p, const double* x, double* y, long n, int level, l
               hipStream_t s) {
   const Filters f = make_filters(p);
   if (n <= kLdsN) {
-    const bool fast = p.M % 2 == 0 && n >= 2 && !std::getenv("JW_FWT_GENERIC");
+    const bool fast = p.M % 2 == 0 && n >= 2 && !knob("JW_FWT_GENERIC");
     for (long b0 = 0; b0 < batch; b0 += 1L << 30) {
       const long nb = batch - b0 < (1L << 30) ? batch - b0 : (1L << 30);
       if (!fast || !launch_fwd2<FMA>(p.M, dim3((unsigned)nb), s, x + b0 * n, y + b0 * n, (int)n,
@@ -1384,7 +1384,7 @@ int reverse_t(const FwtPlan& p, const double* y, double* x, long n, int level, l
   const int steps = log2_exact(n);
   for (int l = level; l < steps; ++l) h0 <<= 1;  // FastWaveletTransform.java:137-141
   if (n <= kLdsN) {
-    const bool fast = p.M % 2 == 0 && n >= 2 && !std::getenv("JW_FWT_GENERIC");
+    const bool fast = p.M % 2 == 0 && n >= 2 && !knob("JW_FWT_GENERIC");
     for (long b0 = 0; b0 < batch; b0 += 1L << 30) {
       const long nb = batch - b0 < (1L << 30) ? batch - b0 : (1L << 30);
       if (!fast || !launch_rev2<FMA>(p.M, dim3((unsigned)nb), s, y + b0 * n, x + b0 * n, (int)n,
@@ -1467,7 +1467,7 @@ int wpt_t(const FwtPlan& p, bool rev, const double* in, double* out, long n, int
   if (rev)
     for (int l = level; l < log2_exact(n); ++l) h0 <<= 1;  // WaveletPacketTransform.java:160-162
   const int lvl_h0 = rev ? (int)h0 : level;
-  if (n <= kLdsN && n >= 2 && p.M % 2 == 0 && !std::getenv("JW_FWT_GENERIC")) {
+  if (n <= kLdsN && n >= 2 && p.M % 2 == 0 && !knob("JW_FWT_GENERIC")) {
     bool ok = true;
     for (long b0 = 0; b0 < batch && ok; b0 += 1L << 30) {
       const long nb = batch - b0 < (1L << 30) ? batch - b0 : (1L << 30);
@@ -1529,11 +1529,11 @@ int wpt_reverse_device(const FwtPlan& p, const double* y, double* x, long n, int
 // disables the strips).  Transform wavelength 2 keeps the reverse's first level at
 // rows >> (lvlM - 1) (FastWaveletTransform.java:137-141).
 int strip_levels(const FwtPlan& p, int rows, int cols, int lvlM) {
-  const char* e = std::getenv("JW_FWT_STRIP");
-  if ((e && e[0] == '0') || std::getenv("JW_FWT_GENERIC")) return 0;
+  const char* e = knob("JW_FWT_STRIP");
+  if ((e && e[0] == '0') || knob("JW_FWT_GENERIC")) return 0;
   if (p.M % 2 || p.M > 20 || p.tw != 2 || cols % kSW || cols > kLdsN || (rows & (rows - 1)))
     return 0;
-  const char* te = std::getenv("JW_FWT_TAIL");
+  const char* te = knob("JW_FWT_TAIL");
   long tail = te ? std::atol(te) : kTailLen;
   if (tail > kTailLen) tail = kTailLen;
   if (tail < 2 * kST) tail = 2 * kST;
@@ -1644,7 +1644,7 @@ int fwt2d_forward_device(const FwtPlan& p, const double* x, double* y, int rows,
                : fwt2d_forward_strips<false>(p, S, x, y, rows, cols, lvlM, lvlN, batch, s);
   }
   const bool fused = p.M % 2 == 0 && rows <= kLdsN && cols <= kLdsN && cols % kLines == 0 &&
-                     rows >= 2 && !std::getenv("JW_FWT_GENERIC");
+                     rows >= 2 && !knob("JW_FWT_GENERIC");
   if (fused) {
     int st = fwt_forward_device(p, x, y, cols, lvlN, rows * batch, s);
     if (st != JW_OK) return st;
@@ -1686,7 +1686,7 @@ int fwt2d_reverse_device(const FwtPlan& p, const double* y, double* x, int rows,
                : fwt2d_reverse_strips<false>(p, S, y, x, rows, cols, lvlM, lvlN, batch, s);
   }
   const bool fused = p.M % 2 == 0 && rows <= kLdsN && cols <= kLdsN && cols % kLines == 0 &&
-                     rows >= 2 && !std::getenv("JW_FWT_GENERIC");
+                     rows >= 2 && !knob("JW_FWT_GENERIC");
   if (fused) {
     long h0 = p.tw;
     for (int l = lvlM; l < log2_exact(rows); ++l) h0 <<= 1;  // FastWaveletTransform.java:137-141
@@ -1730,7 +1730,7 @@ int fwt_columns(const FwtPlan& p, bool rev, const double* in, double* out, int r
     return JW_OK;
   }
   if (p.M % 2 == 0 && rows <= kLdsN && cols % kLines == 0 && cols <= (1L << 30) &&
-      !std::getenv("JW_FWT_GENERIC")) {
+      !knob("JW_FWT_GENERIC")) {
     int arg = lvl;
     if (rev) {  // h0 = tw << (log2 rows - lvl), FastWaveletTransform.java:137-141
       long h0 = p.tw;

@@ -286,7 +286,7 @@ __global__ __launch_bounds__(64) void fwt_cols_stream_rev(const double* __restri
 template <bool FMA>
 bool launch_stream_fwd(int M, int S, hipStream_t s, const double* T, double* y, int rows,
                        int cols, long mat, int batch, const Filters& f) {
-  const char* e = std::getenv("JW_FWT_STREAM");
+  const char* e = knob("JW_FWT_STREAM");
   if ((e && e[0] == '0') || S != 4 || M > kStreamRing || M % 2 || cols % 64) return false;
   const long E = ((1L << S) - 1) * (M - 2);           // look-ahead of the S levels, in rows
   const long trip = (long)kStreamUnroll << S;         // rows per loop trip
@@ -311,7 +311,7 @@ template <bool FMA>
 bool launch_stream_rev(int M, int kind, int S, hipStream_t s, const double* A, long ms_a,
                        const double* y, double* T, int rows, int cols, long mat, int batch,
                        const Filters& f) {
-  const char* e = std::getenv("JW_FWT_STREAM");
+  const char* e = knob("JW_FWT_STREAM");
   if ((e && e[0] == '0') || S != 4 || M > 2 * kRevRing || M % 2 || cols % 64) return false;
   if (!(M == 2 || M == 4 || M == 8 || M == 16) || (kind == JW_WAVELET_HAAR_ORTH && M != 2))
     return false;

@@ -78,6 +78,10 @@ class StreamAllocs {
 
 // Calls in flight hold this shared; jw_release_caches() takes it exclusively, so no call is
 // between looking up a cached table and launching the kernels that read it while it frees.
+// A/B and test settings (JW_*): the environment read once per name, jw_set_knob overrides.
+// The returned string is never freed (nullptr = unset).
+const char* knob(const char* name);
+
 std::shared_mutex& api_mutex();
 void note_device_used(int dev);
 

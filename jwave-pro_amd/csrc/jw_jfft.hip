@@ -79,7 +79,7 @@ int twiddles(long n, bool inverse, int lc1, Tw* out, StreamAllocs& mem, hipStrea
 }
 
 long three_pass_min() {
-  const char* e = std::getenv("JW_JFFT_3PASS_MIN");  // tests: a power of two >= 2^18
+  const char* e = knob("JW_JFFT_3PASS_MIN");  // tests: a power of two >= 2^18
   long m = e ? std::atol(e) : 0;
   if (m < (1L << 18) || (m & (m - 1))) m = 1L << 25;
   return m;
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(256) void kspec_t(const cplx* __restrict__ F, cplx*
 }
 
 bool spect_enabled() {
-  const char* e = std::getenv("JW_AUTO_SPECT");
+  const char* e = knob("JW_AUTO_SPECT");
   return !(e && e[0] == '0');
 }
 
@@ -544,7 +544,7 @@ int modwt_strict(bool inverse, const ModwtPlan& p, const double* in, double* out
   {
     // A/B runs: JW_AUTO_R = the forward pass-1 column length (a power of two, 64 .. 4096,
     // with N / R in the same range)
-    const char* e = std::getenv("JW_AUTO_R");
+    const char* e = knob("JW_AUTO_R");
     const long r = e ? std::atol(e) : 0;
     if (r >= 64 && r <= 4096 && (r & (r - 1)) == 0 && N % r == 0 && N / r >= 64 && N / r <= 4096)
       g.R = r;

@@ -415,7 +415,7 @@ Taps make_taps(const ModwtPlan& p) {
 
 // JW_MODWT_KERNEL=generic forces the runtime-J kernels (A/B and parity testing).
 bool fast_enabled() {
-  const char* e = std::getenv("JW_MODWT_KERNEL");
+  const char* e = knob("JW_MODWT_KERNEL");
   return !(e && std::strcmp(e, "generic") == 0);
 }
 

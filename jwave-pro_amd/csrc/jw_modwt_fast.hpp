@@ -543,7 +543,7 @@ constexpr bool inv_ok() {
 // Threads per workgroup (C = 512 samples per step either way): env JW_FWD_NT / JW_INV_NT
 // (256 or 512) for A/B runs; defaults are the measured best.
 inline int pick_nt(const char* env, int dflt) {
-  const char* e = std::getenv(env);
+  const char* e = knob(env);
   if (e && e[0] == '2') return 256;
   if (e && e[0] == '5') return 512;
   return dflt;
@@ -589,7 +589,7 @@ int launch_fwd(const Taps& t, const double* x, double* c, long N, int batch, hip
   const long npairs = ((seg + warm) / C + 1) / 2;  // an odd extra step runs right of the segment
   const size_t lds = (size_t)G::total * sizeof(double);
   const long cs = (long)(J + 1) * N;
-  const char* g1 = std::getenv("JW_FWD_ONE_RSRC");  // A/B runs: 0 = one resource per row
+  const char* g1 = knob("JW_FWD_ONE_RSRC");  // A/B runs: 0 = one resource per row
   if (cs * 8 < (long)kOOB && !(g1 && g1[0] == '0'))
     return launch(modwt_fwd_fast<L, J, FMA, NT, JW_FWD_SCP, true>, lds, nseg, batch, NT, s, x, N, c, cs, N,
                   seg, warm, npairs, t);
@@ -638,7 +638,7 @@ int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hip
   // The barrier-free kernels are the default wherever they fit: two outputs per lane on the LDS
   // levels (wave2, N even: 16-byte pairs) where inv_prefer2 says so, else one (wave).
   // JW_INV_KERNEL = wave2 / wave / wg forces one of them (A/B runs and the parity tests).
-  const char* w = std::getenv("JW_INV_KERNEL");
+  const char* w = knob("JW_INV_KERNEL");
   const bool force_wg = w && !std::strcmp(w, "wg");
   const bool force_w1 = w && (!std::strcmp(w, "wave") || !std::strcmp(w, "wave1"));
   const bool force_w2 = w && !std::strcmp(w, "wave2");
@@ -651,9 +651,9 @@ int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hip
     if (!force_wg) return wave::launch_inv_wave<L, J, FMA>(t, c, x, N, batch, s);
   }
   constexpr int RF = J >= 7 ? 7 : J + 1;
-  const char* e = std::getenv("JW_INV_RING");
-  const char* top = std::getenv("JW_INV_TOP");
-  const char* ce = std::getenv("JW_INV_C");
+  const char* e = knob("JW_INV_RING");
+  const char* top = knob("JW_INV_TOP");
+  const char* ce = knob("JW_INV_C");
   const bool lds_top = !(top && top[0] == 'g');
   const bool c512 = ce && ce[0] == '5';
   if (e && e[0] == 'o') {

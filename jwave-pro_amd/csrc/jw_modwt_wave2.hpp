@@ -366,7 +366,7 @@ int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hip
   const long ngroups = steps / U;
   const long a_start = (steps - 1) * kS;
   const size_t lds = (size_t)G::lds_doubles * sizeof(double);
-  const char* g1 = std::getenv("JW_INV_ONE_RSRC");  // A/B runs: 0 = one resource per row
+  const char* g1 = knob("JW_INV_ONE_RSRC");  // A/B runs: 0 = one resource per row
   const bool one = (long)(J + 1) * N * 8 < 0x7fffffffL && !(g1 && g1[0] == '0');
   auto kern = one ? modwt_inv_wave2<L, J, FMA, D, U, 1, true> : modwt_inv_wave2<L, J, FMA, D, U>;
   JW_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,

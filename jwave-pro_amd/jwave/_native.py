@@ -45,7 +45,7 @@ JW_WAVELET_HAAR_ORTH = 1
 # tests/test_capi.py::test_library_exports_every_header_symbol).
 EXPORTS = (
     "jw_last_error", "jw_version", "jw_device_count", "jw_set_device", "jw_get_device",
-    "jw_release_caches",
+    "jw_release_caches", "jw_set_knob", "jw_get_knob",
     "jw_modwt_plan_create", "jw_modwt_plan_destroy", "jw_modwt_plan_filters",
     "jw_modwt_forward", "jw_modwt_inverse",
     "jw_fwt_plan_create", "jw_fwt_plan_destroy", "jw_fwt_forward", "jw_fwt_reverse",
@@ -87,6 +87,9 @@ def lib():
     L.jw_get_device.argtypes = [ctypes.POINTER(i)]
     L.jw_release_caches.argtypes = []
     L.jw_release_caches.restype = l
+    L.jw_set_knob.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    L.jw_get_knob.argtypes = [ctypes.c_char_p]
+    L.jw_get_knob.restype = ctypes.c_char_p
     L.jw_modwt_plan_create.argtypes = [ctypes.POINTER(c_dp), c_dp, c_dp, i, i, i]
     L.jw_modwt_plan_destroy.argtypes = [c_dp]
     L.jw_modwt_plan_destroy.restype = None
@@ -117,12 +120,22 @@ def lib():
     L.jw_cwt_fft_scalogram.argtypes = [i, c_dp, c_dp, l, c_dp, i, ctypes.c_double, i, c_dp, i, i,
                                        c_dp]
     non_int = ("jw_last_error", "jw_version", "jw_modwt_plan_destroy", "jw_fwt_plan_destroy",
-               "jw_release_caches")
+               "jw_release_caches", "jw_get_knob")
     for name in EXPORTS:
         if name not in non_int:
             getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
+
+
+def set_knob(name, value):
+    """jw_set_knob: an engine setting (JW_*, A/B runs and tests) for later calls; None = unset."""
+    check(lib().jw_set_knob(name.encode(), None if value is None else str(value).encode()))
+
+
+def get_knob(name):
+    v = lib().jw_get_knob(name.encode())
+    return None if v is None else v.decode()
 
 
 def last_error():

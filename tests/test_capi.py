@@ -36,6 +36,23 @@ def test_library_exports_every_header_symbol():
     assert b"gfx950" in lib.jw_version()
 
 
+def test_knobs_read_once_and_overridable(knobs):
+    # engine settings: the environment's value, read on first use and not again (a setenv after
+    # that changes nothing); jw_set_knob replaces it, None unsets; names outside JW_* refused
+    os.environ["JW_TEST_KNOB_A"] = "7"
+    assert _native.get_knob("JW_TEST_KNOB_A") == "7"
+    os.environ["JW_TEST_KNOB_A"] = "8"
+    assert _native.get_knob("JW_TEST_KNOB_A") == "7"
+    del os.environ["JW_TEST_KNOB_A"]
+    knobs.setenv("JW_TEST_KNOB_A", "9")
+    assert _native.get_knob("JW_TEST_KNOB_A") == "9"
+    knobs.delenv("JW_TEST_KNOB_A")
+    assert _native.get_knob("JW_TEST_KNOB_A") is None
+    assert _native.get_knob("JW_TEST_KNOB_NEVER_SET") is None
+    with pytest.raises(IllegalArgumentException, match="JW_"):
+        _native.set_knob("OMP_NUM_THREADS", "1")
+
+
 def test_jni_glue_binds_only_exported_symbols():
     # jni/jwave_hip_jni.c (no JDK here to compile it): every engine call it makes is a declared,
     # exported C-ABI symbol, and every native method of java/jwave/hip/ has its JNI function

@@ -142,7 +142,7 @@ def test_batch_and_device_tensors(device):
 
 
 @pytest.mark.parametrize("kind", ["morlet", "mexhat", "dog"])
-def test_pipelined_groups_bit_identical(kind, monkeypatch):
+def test_pipelined_groups_bit_identical(kind, knobs):
     # N = 2^18 runs the (signal, scale) inverse FFTs in groups, pass 2 of one group beside
     # pass 1 of the next; an 8 MiB workspace makes groups of 2 pairs (7 groups, last one
     # short).  The pipelined and sequential schedules do the same arithmetic: equal bits.
@@ -152,10 +152,10 @@ def test_pipelined_groups_bit_identical(kind, monkeypatch):
     wv, params = {"morlet": (MorletWavelet(*MORLET6), MORLET6),
                   "mexhat": (MexicanHatWavelet(1.5), (1.5, 0.0)),
                   "dog": (DOGWavelet(3, 0.5), (3.0, 0.5))}[kind]
-    monkeypatch.setenv("JW_CWT_GROUP_MB", "8")
-    monkeypatch.setenv("JW_CWT_PIPE", "1")
+    knobs.setenv("JW_CWT_GROUP_MB", "8")
+    knobs.setenv("JW_CWT_PIPE", "1")
     piped = CWT(wv).transformFFTBatch(xs, scales)
-    monkeypatch.setenv("JW_CWT_PIPE", "0")
+    knobs.setenv("JW_CWT_PIPE", "0")
     seq = CWT(wv).transformFFTBatch(xs, scales)
     assert np.array_equal(piped, seq)
     for b in range(B):
@@ -177,7 +177,7 @@ def test_sinusoid_peaks_at_matching_scale():
 
 @pytest.mark.parametrize("kind", ["morlet", "mexhat"])
 @pytest.mark.parametrize("n", [1 << 13, 1 << 16, 1 << 18, 300001])
-def test_band_scales_one_pass(kind, n, monkeypatch):
+def test_band_scales_one_pass(kind, n, knobs):
     # Scales whose psi_hat band spans few 512-bin blocks run the one-pass band kernel
     # (cwt_band512); JW_CWT_BAND=0 sends every scale through the two-pass FFT.  The band drops
     # only bins below e^-60 of psi_hat's peak, so both agree far inside the oracle tolerance.
@@ -185,10 +185,10 @@ def test_band_scales_one_pass(kind, n, monkeypatch):
     wv, params = {"morlet": (MorletWavelet(*MORLET6), MORLET6),
                   "mexhat": (MexicanHatWavelet(1.5), (1.5, 0.0))}[kind]
     x = orc.fill_uniform(n, 5)
-    monkeypatch.setenv("JW_CWT_INTERP", "0")  # no coarse grids: the band kernel itself
-    monkeypatch.setenv("JW_CWT_BAND", "1000")
+    knobs.setenv("JW_CWT_INTERP", "0")  # no coarse grids: the band kernel itself
+    knobs.setenv("JW_CWT_BAND", "1000")
     band = CWT(wv).transformFFT(x, scales, 1.0).getCoefficients()
-    monkeypatch.setenv("JW_CWT_BAND", "0")
+    knobs.setenv("JW_CWT_BAND", "0")
     two = CWT(wv).transformFFT(x, scales, 1.0).getCoefficients()
     assert nw(band, two) < 1e-13, nw(band, two)
     ex = orc.cwt_fft(x, scales, 1.0, kind, params, 1, exact=True)
@@ -200,7 +200,7 @@ def test_band_scales_one_pass(kind, n, monkeypatch):
 @pytest.mark.parametrize("kind", ["morlet", "mexhat"])
 @pytest.mark.parametrize("n", [1 << 14, 1 << 16, 1 << 18, 300001, 1 << 20])
 @pytest.mark.parametrize("pmin", ["4", "2"])
-def test_coarse_grid_scales(kind, n, pmin, monkeypatch):
+def test_coarse_grid_scales(kind, n, pmin, knobs):
     # Band scales whose band fits a grid of M = N / P points (P >= JW_CWT_INTERP) run as an
     # M-point inverse DFT (the band kernel on the coarse grid, the band divided by the
     # Kaiser-Bessel kernel's transform) and a 19-tap interpolation to the N-point coefficients.
@@ -211,10 +211,10 @@ def test_coarse_grid_scales(kind, n, pmin, monkeypatch):
     wv, params = {"morlet": (MorletWavelet(*MORLET6), MORLET6),
                   "mexhat": (MexicanHatWavelet(1.5), (1.5, 0.0))}[kind]
     x = orc.fill_uniform(n, 11)
-    monkeypatch.setenv("JW_CWT_INTERP", pmin)
+    knobs.setenv("JW_CWT_INTERP", pmin)
     got = CWT(wv).transformFFT(x, scales, 1.0).getCoefficients()
-    monkeypatch.setenv("JW_CWT_INTERP", "0")
-    monkeypatch.setenv("JW_CWT_BAND", "0")
+    knobs.setenv("JW_CWT_INTERP", "0")
+    knobs.setenv("JW_CWT_BAND", "0")
     two = CWT(wv).transformFFT(x, scales, 1.0).getCoefficients()
     for i in range(len(scales)):
         assert nw(got[i], two[i]) < 1e-12, (i, nw(got[i], two[i]))
@@ -225,7 +225,7 @@ def test_coarse_grid_scales(kind, n, pmin, monkeypatch):
             assert nw(got[i], ex[i]) < 1e-11, (i, nw(got[i], ex[i]))
 
 
-def test_coarse_grid_workspace_chunks(monkeypatch):
+def test_coarse_grid_workspace_chunks(knobs):
     # The coarse rows of a group go through a ~128 MB workspace a few signals at a time: at
     # N = 2^18 the P = 4 grids (65536 points) hold 17 signals of 7 scales, so 20 signals take
     # two chunks.  Same values as the two-pass FFT per scale, and the same bits whether the
@@ -238,8 +238,8 @@ def test_coarse_grid_workspace_chunks(monkeypatch):
     got = t.transformFFTBatch(torch.from_numpy(xs).cuda(), scales, 1.0).cpu().numpy()
     one = t.transformFFT(xs[19], scales, 1.0).getCoefficients()
     assert np.array_equal(got[19], one)
-    monkeypatch.setenv("JW_CWT_INTERP", "0")
-    monkeypatch.setenv("JW_CWT_BAND", "0")
+    knobs.setenv("JW_CWT_INTERP", "0")
+    knobs.setenv("JW_CWT_BAND", "0")
     for b in (0, 16, 19):
         two = t.transformFFT(xs[b], scales, 1.0).getCoefficients()
         for i in range(len(scales)):
@@ -247,7 +247,7 @@ def test_coarse_grid_workspace_chunks(monkeypatch):
 
 
 @pytest.mark.parametrize("kind", ["morlet", "mexhat"])
-def test_band_and_pass1_variants_bit_identical(kind, monkeypatch):
+def test_band_and_pass1_variants_bit_identical(kind, knobs):
     # The band kernel's schedules (JW_CWT_BAND_V: load prefetch, one or eight row groups per
     # workgroup at 6 or 4 waves per SIMD) and the two-pass first pass with the X read issued
     # before or after psi_hat's exp (JW_CWT_EARLY) do the same operations: equal bits, at the
@@ -258,8 +258,8 @@ def test_band_and_pass1_variants_bit_identical(kind, monkeypatch):
     x = orc.fill_uniform(n, 9)
     ref = None
     for v, e in [("3", "1"), ("0", "0"), ("2", "1"), ("1", "0")]:
-        monkeypatch.setenv("JW_CWT_BAND_V", v)
-        monkeypatch.setenv("JW_CWT_EARLY", e)
+        knobs.setenv("JW_CWT_BAND_V", v)
+        knobs.setenv("JW_CWT_EARLY", e)
         got = CWT(wv).transformFFT(x, scales, 1.0).getCoefficients()
         if ref is None:
             ref = got
@@ -322,15 +322,14 @@ def test_fft_scalogram_fused(device):
     assert np.array_equal(t.transformFFTScalogram(np.zeros((2, 0)), scales), np.zeros((2, 11)))
 
 
-def test_concurrent_host_threads_with_side_streams(monkeypatch):
+def test_concurrent_host_threads_with_side_streams(knobs):
     # Host arrays (JW_HOST) from four threads at once: each thread stages on its own streams
     # and runs its band and coarse-grid scales on its own side stream (forked from and joined
     # into its staging stream; JW_CWT_OVERLAP=1 forces the side stream, which by default only
     # band-kernel scales take).  Every thread's result equals the same call made alone, bit for
     # bit, and with the side stream off (JW_CWT_OVERLAP=0: the same kernels on one stream).
-    import os
     import threading
-    monkeypatch.setenv("JW_CWT_OVERLAP", "1")
+    knobs.setenv("JW_CWT_OVERLAP", "1")
     n = 1 << 16
     scales = CWT.generateLogScales(2.0, 1024.0, 16)
     xs = [orc.fill_uniform(n, 100 + i) for i in range(4)]
@@ -354,7 +353,7 @@ def test_concurrent_host_threads_with_side_streams(monkeypatch):
     assert not errs, errs
     for i in range(4):
         assert np.array_equal(got[i], alone[i]), i
-    os.environ["JW_CWT_OVERLAP"] = "0"
+    knobs.setenv("JW_CWT_OVERLAP", "0")
     one = CWT(MorletWavelet(*MORLET6)).transformFFT(xs[0], scales, 1.0).getCoefficients()
     assert np.array_equal(one, alone[0])
 

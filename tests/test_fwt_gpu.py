@@ -89,12 +89,12 @@ def test_fwt2d_bit_exact(wname, rows, cols, lvlM, lvlN):
     (4096, 128, 12, 7, None),   # the cfg4 column geometry: levels 1-4 streamed + 256-row tail
     (4096, 64, 4, 3, None),     # exactly the streamed levels: the level-4 approximations final
 ])
-def test_fwt2d_strip_columns_bit_exact(wname, rows, cols, lvlM, lvlN, tail, monkeypatch):
+def test_fwt2d_strip_columns_bit_exact(wname, rows, cols, lvlM, lvlN, tail, knobs):
     # tall matrices run the first column levels as row-strip kernels (4096 rows and filters of
     # up to 16 taps: the one-pass streaming kernel) and the rest in an LDS tail (JW_FWT_TAIL
     # shrinks the tail so small matrices take that path too)
     if tail:
-        monkeypatch.setenv("JW_FWT_TAIL", tail)
+        knobs.setenv("JW_FWT_TAIL", tail)
     wv = W.by_name(wname)
     f = FastWaveletTransform(wv)
     x = orc.fill_uniform(rows * cols, 17).reshape(rows, cols)
@@ -199,7 +199,7 @@ def test_haar_orthogonal_integer_exact():
 
 @pytest.mark.parametrize("wname", ["Haar1", "Daubechies2", "Daubechies8", "Symlet20", "Coiflet5",
                                    "Haar1Orthogonal"])
-def test_fast_and_generic_lds_kernels_agree(wname, monkeypatch):
+def test_fast_and_generic_lds_kernels_agree(wname, knobs):
     # JW_FWT_GENERIC forces the original LDS kernels; both are bit-identical to the oracle
     wv = wavelet(wname)
     f = FastWaveletTransform(wv)
@@ -208,17 +208,17 @@ def test_fast_and_generic_lds_kernels_agree(wname, monkeypatch):
         ref = orc.fwt_forward(x, lvl, wv)
         y_fast = f.forward(x, lvl)
         r_fast = f.reverse(ref, lvl)
-        monkeypatch.setenv("JW_FWT_GENERIC", "1")
+        knobs.setenv("JW_FWT_GENERIC", "1")
         y_gen = f.forward(x, lvl)
         r_gen = f.reverse(ref, lvl)
-        monkeypatch.delenv("JW_FWT_GENERIC")
+        knobs.delenv("JW_FWT_GENERIC")
         rref = orc.fwt_reverse(ref, lvl, wv)
         assert bits_equal(y_fast, ref) and bits_equal(y_gen, ref), (n, lvl)
         assert bits_equal(r_fast, rref) and bits_equal(r_gen, rref), (n, lvl)
 
 
 @pytest.mark.parametrize("wname", CREATE2ARR + ["Haar1Orthogonal", "Legendre1", "Legendre3"])
-def test_row4096_kernels_bit_exact(wname, monkeypatch):
+def test_row4096_kernels_bit_exact(wname, knobs):
     # n = 4096 rows run fwt_fwd_row / fwt_rev_row (compile-time level sizes, wrap copy, details
     # straight to HBM) for filters of up to 20 taps; JW_FWT_ROW=0 runs the runtime-level
     # cascades (which longer filters always use).  STRICT: both bit-identical
@@ -235,10 +235,10 @@ def test_row4096_kernels_bit_exact(wname, monkeypatch):
         assert bits_equal(f.forward(x, lvl), ref), lvl
         assert bits_equal(f.reverse(ref, lvl), rref), lvl
         yf, rf = fm.forward(x, lvl), fm.reverse(ref, lvl)
-        monkeypatch.setenv("JW_FWT_ROW", "0")
+        knobs.setenv("JW_FWT_ROW", "0")
         assert bits_equal(fm.forward(x, lvl), yf), lvl
         assert bits_equal(fm.reverse(ref, lvl), rf), lvl
-        monkeypatch.delenv("JW_FWT_ROW")
+        knobs.delenv("JW_FWT_ROW")
 
 
 @pytest.mark.parametrize("arith", ["strict", "fma"])

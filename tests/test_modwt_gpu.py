@@ -68,7 +68,7 @@ def test_strict_bit_exact_vs_oracle(wname, n, J):
 @pytest.mark.parametrize("wname,n,J", [("Haar1", 4096, 10), ("Daubechies4", 70001, 8),
                                        ("Symlet8", 20000, 6), ("Daubechies8", 3000, 7),
                                        ("Daubechies2", 600, 9), ("Daubechies12", 2048, 6)])
-def test_generic_kernels_bit_exact(wname, n, J, monkeypatch):
+def test_generic_kernels_bit_exact(wname, n, J, knobs):
     # JW_MODWT_KERNEL=generic forces the runtime-J kernels; both paths must agree bit for bit
     wv = W.by_name(wname)
     g, h = ofilters(wv)
@@ -76,7 +76,7 @@ def test_generic_kernels_bit_exact(wname, n, J, monkeypatch):
     ref = orc.modwt_forward(x, J, g, h, "direct_nz")
     m = direct(wv)
     fast = m.forwardMODWT(x, J)
-    monkeypatch.setenv("JW_MODWT_KERNEL", "generic")
+    knobs.setenv("JW_MODWT_KERNEL", "generic")
     gen = m.forwardMODWT(x, J)
     assert bits_equal(gen, ref) and bits_equal(fast, ref)
     assert bits_equal(m.inverseMODWT(ref), orc.modwt_inverse(ref, g, h, "direct_nz"))
@@ -89,7 +89,7 @@ def test_generic_kernels_bit_exact(wname, n, J, monkeypatch):
                                        ("Daubechies8", 30001, 7), ("Daubechies10", 3000, 4),
                                        ("Daubechies4", 1 << 16, 10), ("Daubechies4", 512, 8),
                                        ("Daubechies20", 514, 2), ("Haar1", 600, 2)])
-def test_inverse_kernel_variants_bit_exact(wname, n, J, ring, top, monkeypatch):
+def test_inverse_kernel_variants_bit_exact(wname, n, J, ring, top, knobs):
     # JW_INV_RING=off shifts the history of every level instead of ring-buffering the levels
     # with dilation >= 64; JW_INV_TOP=lds stages level J in LDS instead of reading its taps
     # from global memory; every combination must give the same bits.  n = 512/514 with wide
@@ -97,9 +97,9 @@ def test_inverse_kernel_variants_bit_exact(wname, n, J, ring, top, monkeypatch):
     wv = W.by_name(wname)
     g, h = ofilters(wv)
     c = orc.modwt_forward(orc.fill_uniform(n, 11 + n), J, g, h, "direct_nz")
-    monkeypatch.setenv("JW_INV_KERNEL", "wg")  # these variants are the workgroup kernel's
-    monkeypatch.setenv("JW_INV_RING", ring)
-    monkeypatch.setenv("JW_INV_TOP", top)
+    knobs.setenv("JW_INV_KERNEL", "wg")  # these variants are the workgroup kernel's
+    knobs.setenv("JW_INV_RING", ring)
+    knobs.setenv("JW_INV_TOP", top)
     ref = orc.modwt_inverse(c, g, h, "direct_nz")
     assert bits_equal(direct(wv).inverseMODWT(c), ref)
     xr = direct(wv, arith="fma").inverseMODWT(c)
@@ -111,14 +111,14 @@ def test_inverse_kernel_variants_bit_exact(wname, n, J, ring, top, monkeypatch):
                                        ("Symlet8", 20000, 6), ("Daubechies2", 1000, 9),
                                        ("Daubechies4", 512, 8), ("Daubechies20", 514, 2),
                                        ("Daubechies4", 1 << 16, 10), ("Haar1", 600, 2)])
-def test_inverse_chunk_variants_bit_exact(wname, n, J, chunk, monkeypatch):
+def test_inverse_chunk_variants_bit_exact(wname, n, J, chunk, knobs):
     # JW_INV_C=512: two samples per lane per level (level J from global memory)
     wv = W.by_name(wname)
     g, h = ofilters(wv)
     c = orc.modwt_forward(orc.fill_uniform(n, 13 + n), J, g, h, "direct_nz")
-    monkeypatch.setenv("JW_INV_KERNEL", "wg")
-    monkeypatch.setenv("JW_INV_TOP", "global")
-    monkeypatch.setenv("JW_INV_C", chunk)
+    knobs.setenv("JW_INV_KERNEL", "wg")
+    knobs.setenv("JW_INV_TOP", "global")
+    knobs.setenv("JW_INV_C", chunk)
     ref = orc.modwt_inverse(c, g, h, "direct_nz")
     assert bits_equal(direct(wv).inverseMODWT(c), ref)
     xr = direct(wv, arith="fma").inverseMODWT(c)
@@ -145,7 +145,7 @@ WAVE2_CASES = [
 
 @pytest.mark.parametrize("kernel", ["wave", "wave2", "wg"])
 @pytest.mark.parametrize("wname,n,J", WAVE_CASES + WAVE2_CASES)
-def test_inverse_wave_vs_workgroup_bit_exact(wname, n, J, kernel, monkeypatch):
+def test_inverse_wave_vs_workgroup_bit_exact(wname, n, J, kernel, knobs):
     # one stream per wavefront (no barriers; dilation >= 32 levels in registers, permlane32
     # swaps for dilation 32; wave2: two outputs per lane on the LDS levels) against the
     # workgroup-shared kernel: same bits in both contracts.  Shapes a kernel does not serve
@@ -153,7 +153,7 @@ def test_inverse_wave_vs_workgroup_bit_exact(wname, n, J, kernel, monkeypatch):
     wv = W.by_name(wname)
     g, h = ofilters(wv)
     c = orc.modwt_forward(orc.fill_uniform(n, 17 + n), J, g, h, "direct_nz")
-    monkeypatch.setenv("JW_INV_KERNEL", kernel)
+    knobs.setenv("JW_INV_KERNEL", kernel)
     ref = orc.modwt_inverse(c, g, h, "direct_nz")
     assert bits_equal(direct(wv).inverseMODWT(c), ref)
     xr = direct(wv, arith="fma").inverseMODWT(c)
@@ -168,7 +168,7 @@ def test_inverse_wave_vs_workgroup_bit_exact(wname, n, J, kernel, monkeypatch):
 @pytest.mark.parametrize("one", ["0", "1"])
 @pytest.mark.parametrize("wname,n,J", [("Daubechies4", 1 << 15, 8), ("Symlet8", 70002, 6),
                                        ("Daubechies8", 5000, 7), ("Haar1", 4098, 10)])
-def test_row_resource_forms_bit_exact(wname, n, J, one, monkeypatch):
+def test_row_resource_forms_bit_exact(wname, n, J, one, knobs):
     # The fused kernels address the J + 1 coefficient rows through one buffer resource when
     # they fit (JW_FWD_ONE_RSRC / JW_INV_ONE_RSRC = 1, the default) or one per row (0): the
     # same loads and stores, so both equal the oracle bit for bit (and the tail stores past a
@@ -176,11 +176,11 @@ def test_row_resource_forms_bit_exact(wname, n, J, one, monkeypatch):
     wv = W.by_name(wname)
     g, h = ofilters(wv)
     x = orc.fill_uniform(n, 31 + n)
-    monkeypatch.setenv("JW_FWD_ONE_RSRC", one)
-    monkeypatch.setenv("JW_INV_ONE_RSRC", one)
+    knobs.setenv("JW_FWD_ONE_RSRC", one)
+    knobs.setenv("JW_INV_ONE_RSRC", one)
     ref = orc.modwt_forward(x, J, g, h, "direct_nz")
     for kernel in ("wave2", "wave"):
-        monkeypatch.setenv("JW_INV_KERNEL", kernel)
+        knobs.setenv("JW_INV_KERNEL", kernel)
         m = direct(wv)
         c = m.forwardMODWT(x, J)
         assert bits_equal(c, ref)

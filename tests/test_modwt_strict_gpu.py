@@ -216,8 +216,8 @@ def test_fft_method_bluestein_bit_exact(wname, n, J):
 # fft_rows3) and the unfused long-line MODWT (jw_jfft.hip modwt_strict_long) take over, so they
 # are checked against the oracle at lengths it finishes in seconds; one real 2^25 transform too.
 @pytest.mark.parametrize("n", [1 << 18, 1 << 19, 1 << 20, 1 << 22])
-def test_fft_strict_three_pass_bit_exact(n, monkeypatch):
-    monkeypatch.setenv("JW_JFFT_3PASS_MIN", str(1 << 18))
+def test_fft_strict_three_pass_bit_exact(n, knobs):
+    knobs.setenv("JW_JFFT_3PASS_MIN", str(1 << 18))
     rng = np.random.default_rng(n + 3)
     B = 2 if n <= (1 << 20) else 1
     z = rng.uniform(-1, 1, (B, n)) + 1j * rng.uniform(-1, 1, (B, n))
@@ -238,8 +238,8 @@ LONG_CASES = [("Daubechies4", 1 << 18, 4, 4096, "auto"), ("Symlet8", 1 << 19, 3,
 
 
 @pytest.mark.parametrize("wname,n,J,threshold,method", LONG_CASES)
-def test_modwt_long_lines_bit_exact(wname, n, J, threshold, method, monkeypatch):
-    monkeypatch.setenv("JW_JFFT_3PASS_MIN", str(1 << 18))
+def test_modwt_long_lines_bit_exact(wname, n, J, threshold, method, knobs):
+    knobs.setenv("JW_JFFT_3PASS_MIN", str(1 << 18))
     wv = W.by_name(wname)
     g, h = ofilters(wv)
     xs = np.stack([orc.fill_uniform(n, 5 + b) for b in range(2)])
@@ -254,7 +254,7 @@ def test_modwt_long_lines_bit_exact(wname, n, J, threshold, method, monkeypatch)
         assert bits_equal(xr[b], orc.modwt_inverse(ref, g, h, method, threshold)), b
 
 
-def test_long_lines_workspace_bounded(monkeypatch, device):
+def test_long_lines_workspace_bounded(knobs, device):
     # modwt_strict_long handed its own allocator to every transform, so the
     # three-pass workspaces piled up over batch x levels x transforms (db4 J=8, 8 signals at
     # 2^18: 8 x 56 transforms x 4 MB = 1.8 GB).  Each transform's workspace is now scoped to it:
@@ -262,7 +262,7 @@ def test_long_lines_workspace_bounded(monkeypatch, device):
     import ctypes
     import torch
     from jwave import _native
-    monkeypatch.setenv("JW_JFFT_3PASS_MIN", str(1 << 18))
+    knobs.setenv("JW_JFFT_3PASS_MIN", str(1 << 18))
     n, J, B = 1 << 18, 8, 8
     wv = W.Daubechies4()
     x = torch.empty((B, n), dtype=torch.float64, device=device)
@@ -314,10 +314,10 @@ def test_auto_2_25_forward_bit_exact():
 
 
 @pytest.mark.parametrize("n", [70001, 200001])
-def test_bluestein_three_pass_bit_exact(n, monkeypatch):
+def test_bluestein_three_pass_bit_exact(n, knobs):
     # Bluestein's m-point convolution on three-pass transforms (jw_jfft_bs.hip bs_conv3): the
     # path of non-power-of-two lengths past 2^23 (m > 2^24), at lengths the oracle runs quickly
-    monkeypatch.setenv("JW_JFFT_3PASS_MIN", str(1 << 18))
+    knobs.setenv("JW_JFFT_3PASS_MIN", str(1 << 18))
     rng = np.random.default_rng(n)
     z = rng.uniform(-1, 1, (2, n)) + 1j * rng.uniform(-1, 1, (2, n))
     f = FastFourierTransform()

@@ -26,7 +26,7 @@ def test_wpt_bit_exact_all_wavelets(wname):
 
 
 @pytest.mark.parametrize("wname", ["Haar1", "Daubechies8", "Symlet8", "Haar1Orthogonal"])
-def test_wpt_long_and_generic(wname, monkeypatch):
+def test_wpt_long_and_generic(wname, knobs):
     # n > 4096 runs the per-level global kernels; JW_FWT_GENERIC forces them for n <= 4096 too
     wv = wavelet(wname)
     t = WaveletPacketTransform(wv)
@@ -36,10 +36,10 @@ def test_wpt_long_and_generic(wname, monkeypatch):
         rref = orc.wpt_reverse(ref, lvl, wv)
         assert bits_equal(t.forward(x, lvl), ref)
         assert bits_equal(t.reverse(ref, lvl), rref)
-        monkeypatch.setenv("JW_FWT_GENERIC", "1")
+        knobs.setenv("JW_FWT_GENERIC", "1")
         assert bits_equal(t.forward(x, lvl), ref)
         assert bits_equal(t.reverse(ref, lvl), rref)
-        monkeypatch.delenv("JW_FWT_GENERIC")
+        knobs.delenv("JW_FWT_GENERIC")
 
 
 def test_wpt_batch_device_and_2d(device):
