@@ -161,12 +161,57 @@ typedef double d2 __attribute__((ext_vector_type(2)));
 
 constexpr int kNT2 = 256;               // fast LDS cascades: 4 waves per row
 
+// Outputs (2U, 2U+1) of a multi-wrap level h = H < M, H and U compile-time: for each i
+// ascending the j with (2i + j) mod H == 2U + p are j = p + 2((U - i) mod H/2) + mH ascending
+// (Java's scatter order, M/2 terms per output), so the taps and LDS offsets are constants.
+template <bool FMA, int M, int KIND, int H, int U>
+__device__ __forceinline__ d2 rev_pair_mw(const double* buf, const Filters& f) {
+  constexpr int half = H / 2;
+  double acc[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    double a = 0.;
+#pragma unroll
+    for (int i = 0; i < half; ++i) {
+      const double av = buf[i], dv = buf[i + half];
+      const int s = ((U - i) % half + half) % half;
+#pragma unroll
+      for (int j = p + 2 * s; j < M; j += H) a += contrib<FMA>(av, dv, f.sR[j], f.wR[j], KIND);
+    }
+    acc[p] = a;
+  }
+  return d2{acc[0], acc[1]};
+}
+
+// rev_pair_mw for a runtime pair u < H/2: one compile-time block per u (the level's H/2 lanes
+// take one each).  The predicated form below evaluated all M taps for every i and made the
+// levels h = 2, 4, 8 of the 2-D column tail cost more than its whole memory traffic.
+template <bool FMA, int M, int KIND, int H>
+__device__ __forceinline__ d2 rev_pair_mw_u(const double* buf, int u, const Filters& f) {
+  d2 o = d2{0., 0.};
+  [&]<int... Us>(std::integer_sequence<int, Us...>) {
+    ((u == Us ? (o = rev_pair_mw<FMA, M, KIND, H, Us>(buf, f), 0) : 0), ...);
+  }(std::make_integer_sequence<int, H / 2>{});
+  return o;
+}
+
 // Outputs (2u, 2u+1) that see wrapped taps, in Java's scatter order (i ascending, then j),
 // with compile-time M: fully unrolled, predicated (select, not "+ 0.0") so the sums are
 // bit-identical to the reference's.
 template <bool FMA, int M, int KIND>
 __device__ __forceinline__ d2 rev_pair_wrapped(const double* buf, int h, int u,
                                                const Filters& f) {
+  // multi-wrap levels h = 2 .. 16 as compile-time blocks; FMA only: in STRICT (separate
+  // multiplies, taps as SGPR operands) the blocks pushed the taps into VGPR lanes (~900
+  // v_readlane) and the column tail went 0.79 -> 1.3 ms
+  if constexpr (FMA && M <= 20) {
+    if (h < M) {
+      if (h == 2) return rev_pair_mw_u<FMA, M, KIND, 2>(buf, u, f);
+      if constexpr (M > 4) if (h == 4) return rev_pair_mw_u<FMA, M, KIND, 4>(buf, u, f);
+      if constexpr (M > 8) if (h == 8) return rev_pair_mw_u<FMA, M, KIND, 8>(buf, u, f);
+      if constexpr (M > 16) if (h == 16) return rev_pair_mw_u<FMA, M, KIND, 16>(buf, u, f);
+    }
+  }
   const int half = h >> 1;
   double acc[2];
 #pragma unroll
