@@ -198,9 +198,32 @@ __device__ __forceinline__ d2 rev_pair_mw_u(const double* buf, int u, const Filt
 // Outputs (2u, 2u+1) that see wrapped taps, in Java's scatter order (i ascending, then j),
 // with compile-time M: fully unrolled, predicated (select, not "+ 0.0") so the sums are
 // bit-identical to the reference's.
-template <bool FMA, int M, int KIND>
+template <bool FMA, int M, int KIND, bool ENUM = false>
 __device__ __forceinline__ d2 rev_pair_wrapped(const double* buf, int h, int u,
-                                               const Filters& f) {
+                                               const Filters& f, const d2* tp = nullptr) {
+  // ENUM (STRICT, runtime h: the line cascades): the multi-wrap terms enumerated, M/2 per
+  // output, taps from LDS -- the column tail 789 -> 686 us (profiles/r05/ab/tail_mw); with a
+  // compile-time h (the row kernels) the predicated form below folds better
+  if constexpr (ENUM && !FMA) {
+    if (h < M) {
+      const int half = h >> 1;
+      double acc[2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int k = 2 * u + p;
+        double a = 0.;
+        for (int i = 0; i < half; ++i) {
+          const double av = buf[i], dv = buf[i + half];
+          for (int j = (k - (i << 1)) & (h - 1); j < M; j += h) {
+            const d2 sr = tp[j & ~1], wr = tp[(j & ~1) + 1];
+            a += contrib<FMA>(av, dv, p ? sr.y : sr.x, p ? wr.y : wr.x, KIND);
+          }
+        }
+        acc[p] = a;
+      }
+      return d2{acc[0], acc[1]};
+    }
+  }
   // multi-wrap levels h = 2 .. 16 as compile-time blocks; FMA only: in STRICT (separate
   // multiplies, taps as SGPR operands) the blocks pushed the taps into VGPR lanes (~900
   // v_readlane) and the column tail went 0.79 -> 1.3 ms
@@ -398,7 +421,7 @@ __device__ __forceinline__ void cascade_rev(double* buf, int n, int h0, int tw, 
     }
     if (tid < nslow && !rot_wave && !fma_wrap)
       o[0] = h >= M ? rev_pair_rot<FMA, M, KIND>(buf, h, tid, tp)
-                    : rev_pair_wrapped<FMA, M, KIND>(buf, h, tid, f);
+                    : rev_pair_wrapped<FMA, M, KIND, true>(buf, h, tid, f, tp);
     if (gout && h == n) {
       // last level straight to global memory (lane-consecutive 16-byte stores): no LDS
       // round trip, no barriers; the caller skips its copy-out
