@@ -705,7 +705,11 @@ __device__ __forceinline__ void row_rev_level(double* buf, double* xs, int tid, 
     return;
   }
   if constexpr (H < M) {  // multi-wrap: Java's loop replayed per output
-    if (tid < half) o[0] = rev_pair_wrapped<FMA, M, KIND>(buf, H, tid, f);
+    if constexpr (M <= 20) {  // compile-time blocks per pair (rev_pair_mw), STRICT too here
+      if (tid < half) o[0] = rev_pair_mw_u<FMA, M, KIND, H>(buf, tid, f);
+    } else {
+      if (tid < half) o[0] = rev_pair_wrapped<FMA, M, KIND>(buf, H, tid, f);
+    }
   } else {
 #pragma unroll
     for (int r = 0; r < P; ++r) {
