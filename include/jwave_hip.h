@@ -115,7 +115,12 @@ int jw_modwt_plan_filters(const jw_modwt_plan* plan, double* g, double* h);
  * With a JW_ARITH_STRICT plan (the JVM's arithmetic) every level takes the convolution the
  * reference's performConvolution takes (:640-664): FFT always, DIRECT never, AUTO when the
  * int32 product n * M_j > fftConvolutionThreshold (M_j = (L-1) 2^(j-1) + 1, wrap included).
- * DIRECT levels are bit-identical to circularConvolve (:677-690).  FFT levels run the
+ * DIRECT levels are bit-identical to circularConvolve (:677-690), non-finite data included:
+ * like the reference, which multiplies the up-sampled zero taps too (upsample :618-630), an
+ * output whose window holds a +-Inf or NaN sample on a zero tap is NaN (0 * Inf = NaN); the
+ * engine flags signals with non-finite values on the device and re-runs only those through a
+ * zero-tap pass on the same stream (JW_DEVICE stays asynchronous; FMA plans get the same NaN
+ * pattern).  FFT levels run the
  * reference's circularConvolveFFT (:752-786) with its own FFT: radix 2 with recurrence
  * twiddles for powers of two (FastFourierTransform.java:172-212) and its Bluestein transform for
  * other lengths (:259-324), both bit-identical to the JVM for power-of-two n <= 2^28 and other

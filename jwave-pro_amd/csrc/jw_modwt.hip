@@ -11,6 +11,17 @@
 // ascending order, starting from +0.0, without FMA (JW_ARITH_STRICT): the JVM's exact
 // IEEE sequence for finite inputs.
 //
+// Non-finite inputs.  Java multiplies the zero taps too, and 0 * +-Inf = 0 * NaN = NaN, so an
+// output whose window holds a non-finite sample on a zero tap is NaN in JWave; otherwise the
+// zero taps add +-0 and the non-zero-tap sum stands.  Level by level, that is exactly the
+// reference (checked against the faithful every-tap oracle, tests/test_modwt_nonfinite_gpu.py).
+// The fast paths skip the zero taps and flag a signal whose final row holds a non-finite value
+// (fast::nonfinite_flag: a non-finite sample anywhere in the cascade reaches that row); the
+// generic streaming kernel then runs again for the flagged signals only, in FIX mode, which
+// adds the zero-tap test to every output (modwt_fwd_fused / modwt_inv_fused <.., true>).  The
+// per-level kernels test the zero taps themselves when their input row is flagged.  All of it
+// stays on the stream: a clean signal costs a flag word, a memset and an early-exit launch.
+//
 // Design (DESIGN.md "MODWT kernels"): one workgroup streams a segment of one signal through
 // all J levels in LDS.  The signal is walked in chunks of C samples; every level keeps the
 // (L-1)*2^(j-1) samples of history its dilated filter needs in an LDS buffer, so each
@@ -54,6 +65,63 @@ __device__ __forceinline__ long wrap(long p, long N) {
 
 __host__ __device__ constexpr long hist_of(int L, int j) { return (long)(L - 1) << (j - 1); }
 
+// True when a zero tap of the up-sampled window at p meets a non-finite sample: taps m in
+// [1, M) with m mod d != 0, at p[-m] (circularConvolve, DIR = -1) or p[+m] (adjoint, +1).
+// Literal walk over the window in LDS (FIX mode only).
+template <int DIR>
+__device__ __forceinline__ bool zero_tap_nonfinite(const double* p, int d, int M) {
+  bool hit = false;
+  if (d > 1) {
+    for (int m = 1; m < M; ++m)
+      if ((m & (d - 1)) != 0) hit |= !__builtin_isfinite(p[DIR * m]);
+  }
+  return hit;
+}
+
+// The same test for the per-level kernels, whose window lives in global memory (M up to
+// 39 * 4096 + 1): a wave covers outputs n0 .. n0 + 63 (lane l: n = n0 + l) and walks the union
+// of their windows 64 positions at a time; each non-finite position found (ballot) is checked
+// against every lane's window.  ADJ: window n .. n + M - 1, else n - M + 1 .. n.  Every lane
+// of the wave must take part (dead tail lanes included).
+template <bool ADJ>
+__device__ bool zero_tap_nonfinite_wave(const double* v, long N, long n, long M, long d) {
+  const int lane = threadIdx.x & 63;
+  const long n0 = n - lane;
+  const long lo = ADJ ? n0 : n0 - (M - 1);
+  const long hi = ADJ ? n0 + 63 + (M - 1) : n0 + 63;
+  bool hit = false;
+  for (long base = lo; base <= hi; base += 64) {
+    const long q = base + lane;
+    const bool bad = q <= hi && !__builtin_isfinite(v[wrap(q, N)]);
+    unsigned long long mask = __ballot(bad);
+    while (mask != 0) {
+      const int b = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      const long m = ADJ ? (base + b) - n : n - (base + b);
+      if (m > 0 && m < M && (m & (d - 1)) != 0) hit = true;
+    }
+  }
+  return hit;
+}
+
+constexpr double kNaN = __builtin_nan("");
+
+// flags[r * fstride + b] = 1 when row r of signal b holds a non-finite value (rows r < nrows at
+// row_stride within a signal, signals at sig_stride).  Vector stores of the constant 1.
+__global__ __launch_bounds__(256) void modwt_nonfinite_rows(const double* __restrict__ p,
+                                                            long sig_stride, long row_stride,
+                                                            int nrows, long N,
+                                                            int* __restrict__ flags,
+                                                            long fstride) {
+  const double* ps = p + (long)blockIdx.y * sig_stride;
+  for (int r = 0; r < nrows; ++r) {
+    bool bad = false;
+    for (long n = (long)blockIdx.x * 256 + threadIdx.x; n < N; n += (long)gridDim.x * 256)
+      bad |= !__builtin_isfinite(ps[(long)r * row_stride + n]);
+    if (bad) flags[(long)r * fstride + blockIdx.y] = 1;
+  }
+}
+
 // Flat history index e -> level j (1-based): level j owns e in [(L-1)(2^(j-1)-1), (L-1)(2^j-1)).
 template <int L>
 __device__ __forceinline__ int level_of(int e) {
@@ -66,11 +134,18 @@ __device__ __forceinline__ int level_of(int e) {
 // stream positions [a - hist_j, a + C).  After the J levels of a step, the last hist_j
 // samples of every buffer move to its front (the history of the next chunk).
 // B_{j-1} starts at (L-1)(2^(j-1)-1) + (j-1)*C.
+// FIX = false: the generic path; nf (nullable) receives the signal's non-finite flag.
+// FIX = true: the zero-tap pass; only signals whose nf is set run, every output gets the
+// zero-tap test (NaN on a hit), and all rows of the signal are rewritten.
 // ---------------------------------------------------------------------------------------
-template <int L, bool FMA>
+template <int L, bool FMA, bool FIX>
 __global__ __launch_bounds__(kNT) void modwt_fwd_fused(const double* __restrict__ x,
                                                        double* __restrict__ coeffs, long N, int J,
-                                                       long seg_len, long warm, Taps taps) {
+                                                       long seg_len, long warm, Taps taps,
+                                                       int* __restrict__ nf) {
+  if constexpr (FIX) {
+    if (nf[blockIdx.y] == 0) return;  // workgroup-uniform: a clean signal
+  }
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int tid = threadIdx.x;
   const long P = (long)blockIdx.x * seg_len;
@@ -82,6 +157,7 @@ __global__ __launch_bounds__(kNT) void modwt_fwd_fused(const double* __restrict_
   for (int i = tid; i < total; i += kNT) lds[i] = 0.0;
 
   double pre[kLoad];
+  bool bad = false;
   long a = P - warm;
   {
     const long base = wrap(a, N);
@@ -118,11 +194,18 @@ __global__ __launch_bounds__(kNT) void modwt_fwd_fused(const double* __restrict_
       double* VJ = cs + (long)J * N;
       const bool last = (j == J);
       auto emit = [&](int i, double w, double v) {
+        if constexpr (FIX) {
+          if (zero_tap_nonfinite<-1>(src + hist + i, d, hist + 1)) w = v = kNaN;
+        }
         const long pos = a + i;
         const bool keep = pos >= P && pos < seg_end;
         if (keep) W[pos] = w;
-        if (!last) dst[i] = v;
-        else if (keep) VJ[pos] = v;
+        if (!last) {
+          dst[i] = v;
+        } else {
+          if (keep) VJ[pos] = v;
+          bad |= !__builtin_isfinite(v);
+        }
       };
       if (2 * d <= kC) {
         // Pair (i1, i1+d): the two outputs share L-1 of their L taps -> L+1 LDS reads.
@@ -180,6 +263,7 @@ __global__ __launch_bounds__(kNT) void modwt_fwd_fused(const double* __restrict_
       }
     }
   }
+  if constexpr (!FIX) fast::nonfinite_flag(nf, bad);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -187,10 +271,14 @@ __global__ __launch_bounds__(kNT) void modwt_fwd_fused(const double* __restrict_
 // [a, a + C + hist_j) (VB_j starts at (j-1)*C + (L-1)(2^(j-1)-1)), then two W staging
 // buffers of C + hist_J samples.
 // ---------------------------------------------------------------------------------------
-template <int L, bool FMA>
+template <int L, bool FMA, bool FIX>
 __global__ __launch_bounds__(kNT) void modwt_inv_fused(const double* __restrict__ coeffs,
                                                        double* __restrict__ x, long N, int J,
-                                                       long seg_len, long warm, Taps taps) {
+                                                       long seg_len, long warm, Taps taps,
+                                                       int* __restrict__ nf) {
+  if constexpr (FIX) {
+    if (nf[blockIdx.y] == 0) return;
+  }
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int tid = threadIdx.x;
   const long P = (long)blockIdx.x * seg_len;
@@ -210,6 +298,7 @@ __global__ __launch_bounds__(kNT) void modwt_inv_fused(const double* __restrict_
   const long steps = nchunks + warm / kC;
   double pre[kLoad];
   double wreg[kWinPer];
+  bool bad = false;
 
   auto load_chunk = [&](const double* row, long a0) {
     const long base = wrap(a0, N);
@@ -264,11 +353,18 @@ __global__ __launch_bounds__(kNT) void modwt_inv_fused(const double* __restrict_
       if (j > 1) load_window(j - 1, a);  // in flight during this level's arithmetic
       double* vdst = (j > 1) ? vb(j - 1) : nullptr;
       auto emit = [&](int i, double v) {
+        if constexpr (FIX) {
+          // vFromApprox and vFromDetail (:366-369) are NaN on a zero-tap hit of their window
+          if (zero_tap_nonfinite<1>(vsrc + i, d, (L - 1) * d + 1) ||
+              zero_tap_nonfinite<1>(wsrc + i, d, (L - 1) * d + 1))
+            v = kNaN;
+        }
         if (j > 1) {
           vdst[i] = v;
         } else {
           const long pos = a + i;
           if (pos >= P && pos < seg_end) xs[pos] = v;
+          bad |= !__builtin_isfinite(v);
         }
       };
       if (2 * d <= kC) {
@@ -326,53 +422,80 @@ __global__ __launch_bounds__(kNT) void modwt_inv_fused(const double* __restrict_
     }
     __syncthreads();
   }
+  if constexpr (!FIX) fast::nonfinite_flag(nf, bad);
 }
 
 // ---------------------------------------------------------------------------------------
 // Per-level kernels: any N, L, J (used when the fused buffers exceed the LDS budget).
 // ---------------------------------------------------------------------------------------
+// fin (nullable): per-signal flag "the input row holds a non-finite value"; when set, every
+// output gets the zero-tap test.  fout (nullable): set when the V output holds one.
 template <int L, bool FMA>
 __global__ __launch_bounds__(kNT) void modwt_fwd_level(const double* __restrict__ v, long v_stride,
                                                        double* __restrict__ w, long w_stride,
                                                        double* __restrict__ vn, long vn_stride,
-                                                       long N, long d, Taps taps) {
+                                                       long N, long d, Taps taps,
+                                                       const int* __restrict__ fin,
+                                                       int* __restrict__ fout) {
   const long n = (long)blockIdx.x * kNT + threadIdx.x;
-  if (n >= N) return;
+  const bool live = n < N;  // dead tail lanes stay for the wave-wide zero-tap walk
+  const long nn = live ? n : N - 1;
   const double* vs = v + (long)blockIdx.y * v_stride;
   double wa = 0.0, ga = 0.0;
 #pragma unroll
   for (int m = 0; m < L; ++m) {
-    const double xv = vs[wrap(n - m * d, N)];
+    const double xv = vs[wrap(nn - m * d, N)];
     wa = madd<FMA>(wa, taps.b[m], xv);
     ga = madd<FMA>(ga, taps.a[m], xv);
   }
+  if (fin != nullptr && fin[blockIdx.y] != 0) {
+    if (zero_tap_nonfinite_wave<false>(vs, N, n, (long)(L - 1) * d + 1, d)) wa = ga = kNaN;
+  }
+  if (!live) return;
   w[(long)blockIdx.y * w_stride + n] = wa;
   vn[(long)blockIdx.y * vn_stride + n] = ga;
+  if (fout != nullptr && !__builtin_isfinite(ga)) fout[blockIdx.y] = 1;
 }
 
+// fa / fb (nullable): flags of the V_j / W_j input rows; fout: set when the output holds a
+// non-finite value.
 template <int L, bool FMA>
 __global__ __launch_bounds__(kNT) void modwt_inv_level(const double* __restrict__ v, long v_stride,
                                                        const double* __restrict__ w, long w_stride,
                                                        double* __restrict__ out, long out_stride,
-                                                       long N, long d, Taps taps) {
+                                                       long N, long d, Taps taps,
+                                                       const int* __restrict__ fa,
+                                                       const int* __restrict__ fb,
+                                                       int* __restrict__ fout) {
   const long n = (long)blockIdx.x * kNT + threadIdx.x;
-  if (n >= N) return;
+  const bool live = n < N;
+  const long nn = live ? n : N - 1;
   const double* vs = v + (long)blockIdx.y * v_stride;
   const double* ws = w + (long)blockIdx.y * w_stride;
   double ap = 0.0, dp = 0.0;
 #pragma unroll
   for (int m = 0; m < L; ++m) {
-    const long idx = wrap(n + m * d, N);
+    const long idx = wrap(nn + m * d, N);
     ap = madd<FMA>(ap, taps.a[m], vs[idx]);
     dp = madd<FMA>(dp, taps.b[m], ws[idx]);
   }
-  out[(long)blockIdx.y * out_stride + n] = ap + dp;
+  double o = ap + dp;
+  if ((fa != nullptr && fa[blockIdx.y] != 0) || (fb != nullptr && fb[blockIdx.y] != 0)) {
+    const long M = (long)(L - 1) * d + 1;
+    const bool hv = zero_tap_nonfinite_wave<true>(vs, N, n, M, d);
+    const bool hw = zero_tap_nonfinite_wave<true>(ws, N, n, M, d);
+    if (hv || hw) o = kNaN;
+  }
+  if (!live) return;
+  out[(long)blockIdx.y * out_stride + n] = o;
+  if (fout != nullptr && !__builtin_isfinite(o)) fout[blockIdx.y] = 1;
 }
 
 // ---------------------------------------------------------------------------------------
 // Host-side dispatch
 // ---------------------------------------------------------------------------------------
 constexpr size_t kMaxFusedLds = 80 * 1024;
+constexpr size_t kMaxFixLds = 160 * 1024;  // the zero-tap pass may take a CU's whole LDS
 
 size_t fused_lds_bytes(int L, int J, bool inverse) {
   const long H = (long)(L - 1) * ((1L << J) - 1);
@@ -381,12 +504,15 @@ size_t fused_lds_bytes(int L, int J, bool inverse) {
   return (size_t)doubles * sizeof(double);
 }
 
-bool fused_ok(int L, int J, bool inverse) {
+bool fused_fits(int L, int J, bool inverse, size_t max_lds) {
   const long H = (long)(L - 1) * ((1L << J) - 1);
   if (H > kHistMax) return false;
   if (inverse && kC + hist_of(L, J) > kWinMax) return false;
-  return fused_lds_bytes(L, J, inverse) <= kMaxFusedLds;
+  return fused_lds_bytes(L, J, inverse) <= max_lds;
 }
+bool fused_ok(int L, int J, bool inverse) { return fused_fits(L, J, inverse, kMaxFusedLds); }
+// The streaming kernels (fast or generic) may run only where their zero-tap pass can follow.
+bool fix_ok(int L, int J, bool inverse) { return fused_fits(L, J, inverse, kMaxFixLds); }
 
 // Segment length: whole chunks, long enough that the warm-up is a small fraction, short
 // enough that the grid has several workgroups per CU.
@@ -420,12 +546,12 @@ bool fast_enabled() {
 }
 
 int try_fast_forward(int L, const Taps& t, bool fma, const double* x, double* c, long N, int J,
-                     int B, hipStream_t s) {
+                     int B, hipStream_t s, int* nf) {
   if (!fast_enabled()) return fast::kNotHandled;
   switch (L) {
 #define JW_CASE(LL) \
   case LL:          \
-    return fast::forward<LL>(t, fma, x, c, N, J, B, s);
+    return fast::forward<LL>(t, fma, x, c, N, J, B, s, nf);
     JW_FAST_LENGTHS(JW_CASE)
 #undef JW_CASE
     default:
@@ -434,12 +560,12 @@ int try_fast_forward(int L, const Taps& t, bool fma, const double* x, double* c,
 }
 
 int try_fast_inverse(int L, const Taps& t, bool fma, const double* c, double* x, long N, int J,
-                     int B, hipStream_t s) {
+                     int B, hipStream_t s, int* nf) {
   if (!fast_enabled()) return fast::kNotHandled;
   switch (L) {
 #define JW_CASE(LL) \
   case LL:          \
-    return fast::inverse<LL>(t, fma, c, x, N, J, B, s);
+    return fast::inverse<LL>(t, fma, c, x, N, J, B, s, nf);
     JW_FAST_LENGTHS(JW_CASE)
 #undef JW_CASE
     default:
@@ -447,47 +573,114 @@ int try_fast_inverse(int L, const Taps& t, bool fma, const double* c, double* x,
   }
 }
 
+// `count` zeroed per-signal flag words, stream-ordered.
+int alloc_flags(StreamAllocs& mem, int** f, size_t count, hipStream_t s) {
+  JW_HIP_TRY(mem.alloc(f, count * sizeof(int)));
+  JW_HIP_TRY(hipMemsetAsync(*f, 0, count * sizeof(int), s));
+  return JW_OK;
+}
+
+// flags[r * batch + b] for rows r0 .. r0 + nrows - 1 of every signal (signal stride sig).
+int scan_rows(const double* p, long sig, long row_stride, int nrows, long N, int batch,
+              int* flags, hipStream_t s) {
+  long gx = (N + 255) / 256;
+  const long want = 4096 / (batch > 0 ? batch : 1);
+  if (gx > want) gx = want < 1 ? 1 : want;
+  for (int b0 = 0; b0 < batch; b0 += 65535) {
+    const int nb = batch - b0 < 65535 ? batch - b0 : 65535;
+    hipLaunchKernelGGL(modwt_nonfinite_rows, dim3((unsigned)gx, (unsigned)nb), dim3(256), 0, s,
+                       p + (long)b0 * sig, sig, row_stride, nrows, N, flags + b0, (long)batch);
+  }
+  JW_HIP_TRY(hipGetLastError());
+  return JW_OK;
+}
+
+// The generic streaming kernels, main (FIX = false, nf = out flags or null) or zero-tap pass.
+template <int L, bool FMA, bool FIX>
+int launch_fused_fwd(const Taps& t, const double* x, double* coeffs, long N, int J, int batch,
+                     int* nf, hipStream_t s) {
+  const size_t lds = fused_lds_bytes(L, J, false);
+  const long H = (long)(L - 1) * ((1L << J) - 1);
+  const long warm = ((H + kC - 1) / kC) * kC;
+  const long seg = pick_segment(N, batch, warm);
+  const long nseg = (N + seg - 1) / seg;
+  const long rstride = (long)(J + 1) * N;
+  auto kern = modwt_fwd_fused<L, FMA, FIX>;
+  JW_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)lds));
+  for (int b0 = 0; b0 < batch; b0 += 65535) {
+    const int nb = batch - b0 < 65535 ? batch - b0 : 65535;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nseg, (unsigned)nb), dim3(kNT), lds, s,
+                       x + (long)b0 * N, coeffs + (long)b0 * rstride, N, J, seg, warm, t,
+                       nf ? nf + b0 : nullptr);
+  }
+  JW_HIP_TRY(hipGetLastError());
+  return JW_OK;
+}
+
+template <int L, bool FMA, bool FIX>
+int launch_fused_inv(const Taps& t, const double* coeffs, double* x, long N, int J, int batch,
+                     int* nf, hipStream_t s) {
+  const size_t lds = fused_lds_bytes(L, J, true);
+  const long H = (long)(L - 1) * ((1L << J) - 1);
+  const long warm = ((H + kC - 1) / kC) * kC;
+  const long seg = pick_segment(N, batch, warm);
+  const long nseg = (N + seg - 1) / seg;
+  const long rstride = (long)(J + 1) * N;
+  auto kern = modwt_inv_fused<L, FMA, FIX>;
+  JW_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)lds));
+  for (int b0 = 0; b0 < batch; b0 += 65535) {
+    const int nb = batch - b0 < 65535 ? batch - b0 : 65535;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nseg, (unsigned)nb), dim3(kNT), lds, s,
+                       coeffs + (long)b0 * rstride, x + (long)b0 * N, N, J, seg, warm, t,
+                       nf ? nf + b0 : nullptr);
+  }
+  JW_HIP_TRY(hipGetLastError());
+  return JW_OK;
+}
+
 template <int L, bool FMA>
 int forward_impl(const ModwtPlan& p, const double* x, double* coeffs, long N, int J, int batch,
                  hipStream_t s) {
   const Taps t = make_taps<L>(p);
   const long rstride = (long)(J + 1) * N;
-  if (int st = try_fast_forward(L, t, FMA, x, coeffs, N, J, batch, s); st != fast::kNotHandled)
-    return st;
-  if (fused_ok(L, J, false)) {
-    const size_t lds = fused_lds_bytes(L, J, false);
-    const long H = (long)(L - 1) * ((1L << J) - 1);
-    const long warm = ((H + kC - 1) / kC) * kC;
-    const long seg = pick_segment(N, batch, warm);
-    const long nseg = (N + seg - 1) / seg;
-    auto kern = modwt_fwd_fused<L, FMA>;
-    JW_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)lds));
-    for (int b0 = 0; b0 < batch; b0 += 65535) {
-      const int nb = batch - b0 < 65535 ? batch - b0 : 65535;
-      hipLaunchKernelGGL(kern, dim3((unsigned)nseg, (unsigned)nb), dim3(kNT), lds, s,
-                         x + (long)b0 * N, coeffs + (long)b0 * rstride, N, J, seg, warm, t);
+  StreamAllocs mem(s);
+  const bool zt = J >= 2 && L > 1;  // level 1 has no zero taps
+  if (!zt || fix_ok(L, J, false)) {
+    int* nf = nullptr;
+    if (zt) {
+      if (int st = alloc_flags(mem, &nf, (size_t)batch, s); st != JW_OK) return st;
     }
-    JW_HIP_TRY(hipGetLastError());
-    return JW_OK;
+    int st = try_fast_forward(L, t, FMA, x, coeffs, N, J, batch, s, nf);
+    if (st == fast::kNotHandled && fused_ok(L, J, false))
+      st = launch_fused_fwd<L, FMA, false>(t, x, coeffs, N, J, batch, nf, s);
+    if (st != fast::kNotHandled) {
+      if (st != JW_OK || !zt) return st;
+      return launch_fused_fwd<L, FMA, true>(t, x, coeffs, N, J, batch, nf, s);
+    }
   }
   // Per-level path: V_j ping-pongs between coefficient row J and a workspace row so that
-  // V_J lands in row J.
+  // V_J lands in row J.  fl[j] = "V_j of the signal holds a non-finite value".
   double* tmp = nullptr;
-  StreamAllocs mem(s);
+  int* fl = nullptr;
   JW_HIP_TRY(mem.alloc(&tmp, sizeof(double) * (size_t)N * batch));
+  if (int st = alloc_flags(mem, &fl, (size_t)(J + 1) * batch, s); st != JW_OK) return st;
   const double* vin = x;
   long vin_stride = N;
   for (int j = 1; j <= J; ++j) {
     const bool to_row = ((J - j) % 2) == 0;
     double* vout = to_row ? coeffs + (long)J * N : tmp;
     const long vout_stride = to_row ? rstride : N;
+    const int* fin = j >= 2 ? fl + (long)(j - 1) * batch : nullptr;
+    int* fout = j < J ? fl + (long)j * batch : nullptr;
     for (int b0 = 0; b0 < batch; b0 += 65535) {
       const int nb = batch - b0 < 65535 ? batch - b0 : 65535;
       dim3 grid((unsigned)((N + kNT - 1) / kNT), (unsigned)nb);
       hipLaunchKernelGGL((modwt_fwd_level<L, FMA>), grid, dim3(kNT), 0, s, vin + b0 * vin_stride,
                          vin_stride, coeffs + (long)(j - 1) * N + b0 * rstride, rstride,
-                         vout + b0 * vout_stride, vout_stride, N, 1L << (j - 1), t);
+                         vout + b0 * vout_stride, vout_stride, N, 1L << (j - 1), t,
+                         fin ? fin + b0 : nullptr, fout ? fout + b0 : nullptr);
     }
     JW_HIP_TRY(hipGetLastError());
     vin = vout;
@@ -501,39 +694,44 @@ int inverse_impl(const ModwtPlan& p, const double* coeffs, double* x, long N, in
                  hipStream_t s) {
   const Taps t = make_taps<L>(p);
   const long rstride = (long)(J + 1) * N;
-  if (int st = try_fast_inverse(L, t, FMA, coeffs, x, N, J, batch, s); st != fast::kNotHandled)
-    return st;
-  if (fused_ok(L, J, true)) {
-    const size_t lds = fused_lds_bytes(L, J, true);
-    const long H = (long)(L - 1) * ((1L << J) - 1);
-    const long warm = ((H + kC - 1) / kC) * kC;
-    const long seg = pick_segment(N, batch, warm);
-    const long nseg = (N + seg - 1) / seg;
-    auto kern = modwt_inv_fused<L, FMA>;
-    JW_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)lds));
-    for (int b0 = 0; b0 < batch; b0 += 65535) {
-      const int nb = batch - b0 < 65535 ? batch - b0 : 65535;
-      hipLaunchKernelGGL(kern, dim3((unsigned)nseg, (unsigned)nb), dim3(kNT), lds, s,
-                         coeffs + (long)b0 * rstride, x + (long)b0 * N, N, J, seg, warm, t);
-    }
-    JW_HIP_TRY(hipGetLastError());
-    return JW_OK;
-  }
-  double* tmp = nullptr;
   StreamAllocs mem(s);
+  const bool zt = J >= 2 && L > 1;
+  if (!zt || fix_ok(L, J, true)) {
+    int* nf = nullptr;
+    if (zt) {
+      if (int st = alloc_flags(mem, &nf, (size_t)batch, s); st != JW_OK) return st;
+    }
+    int st = try_fast_inverse(L, t, FMA, coeffs, x, N, J, batch, s, nf);
+    if (st == fast::kNotHandled && fused_ok(L, J, true))
+      st = launch_fused_inv<L, FMA, false>(t, coeffs, x, N, J, batch, nf, s);
+    if (st != fast::kNotHandled) {
+      if (st != JW_OK || !zt) return st;
+      return launch_fused_inv<L, FMA, true>(t, coeffs, x, N, J, batch, nf, s);
+    }
+  }
+  // Per-level path.  fr[r] = "coefficient row r holds a non-finite value" (one scan),
+  // fv[j] = "V_j (level j+1's output) does".
+  double* tmp = nullptr;
+  int *fr = nullptr, *fv = nullptr;
   JW_HIP_TRY(mem.alloc(&tmp, sizeof(double) * (size_t)N * batch));
+  if (int st = alloc_flags(mem, &fr, (size_t)(2 * J + 1) * batch, s); st != JW_OK) return st;
+  fv = fr + (long)(J + 1) * batch - (long)batch;  // fv[j] at fv + j*batch, j = 1..J-1
+  if (int st = scan_rows(coeffs, rstride, N, J + 1, N, batch, fr, s); st != JW_OK) return st;
   const double* vin = coeffs + (long)J * N;
   long vin_stride = rstride;
   for (int j = J; j >= 1; --j) {
     const bool to_out = ((j - 1) % 2) == 0;
     double* vout = to_out ? x : tmp;
+    const int* fa = j == 1 ? nullptr : j == J ? fr + (long)J * batch : fv + (long)j * batch;
+    const int* fb = j == 1 ? nullptr : fr + (long)(j - 1) * batch;
+    int* fout = j > 1 ? fv + (long)(j - 1) * batch : nullptr;
     for (int b0 = 0; b0 < batch; b0 += 65535) {
       const int nb = batch - b0 < 65535 ? batch - b0 : 65535;
       dim3 grid((unsigned)((N + kNT - 1) / kNT), (unsigned)nb);
       hipLaunchKernelGGL((modwt_inv_level<L, FMA>), grid, dim3(kNT), 0, s, vin + b0 * vin_stride,
                          vin_stride, coeffs + (long)(j - 1) * N + b0 * rstride, rstride,
-                         vout + b0 * N, N, N, 1L << (j - 1), t);
+                         vout + b0 * N, N, N, 1L << (j - 1), t, fa ? fa + b0 : nullptr,
+                         fb ? fb + b0 : nullptr, fout ? fout + b0 : nullptr);
     }
     JW_HIP_TRY(hipGetLastError());
     vin = vout;
@@ -576,15 +774,24 @@ int inverse_dispatch(const ModwtPlan& p, const double* c, double* x, long N, int
   }
 }
 
+// One DIRECT level of the AUTO / STRICT level schedule (jw_jfft*.hip): its input rows may come
+// from an FFT level, so they are scanned for non-finite values first (levels >= 2 only).
 template <int L, bool FMA>
 int level_forward(const ModwtPlan& p, int j, const double* v, long vs, double* w, long ws,
                   double* vn, long vns, long N, int batch, hipStream_t s) {
   const Taps t = make_taps<L>(p);
+  StreamAllocs mem(s);
+  int* fin = nullptr;
+  if (j >= 2 && L > 1) {
+    if (int st = alloc_flags(mem, &fin, (size_t)batch, s); st != JW_OK) return st;
+    if (int st = scan_rows(v, vs, 0, 1, N, batch, fin, s); st != JW_OK) return st;
+  }
   for (int b0 = 0; b0 < batch; b0 += 65535) {
     const int nb = batch - b0 < 65535 ? batch - b0 : 65535;
     dim3 grid((unsigned)((N + kNT - 1) / kNT), (unsigned)nb);
     hipLaunchKernelGGL((modwt_fwd_level<L, FMA>), grid, dim3(kNT), 0, s, v + b0 * vs, vs,
-                       w + b0 * ws, ws, vn + b0 * vns, vns, N, 1L << (j - 1), t);
+                       w + b0 * ws, ws, vn + b0 * vns, vns, N, 1L << (j - 1), t,
+                       fin ? fin + b0 : nullptr, nullptr);
   }
   JW_HIP_TRY(hipGetLastError());
   return JW_OK;
@@ -594,11 +801,19 @@ template <int L, bool FMA>
 int level_inverse(const ModwtPlan& p, int j, const double* v, long vs, const double* w, long ws,
                   double* out, long os, long N, int batch, hipStream_t s) {
   const Taps t = make_taps<L>(p);
+  StreamAllocs mem(s);
+  int* f = nullptr;
+  if (j >= 2 && L > 1) {
+    if (int st = alloc_flags(mem, &f, (size_t)2 * batch, s); st != JW_OK) return st;
+    if (int st = scan_rows(v, vs, 0, 1, N, batch, f, s); st != JW_OK) return st;
+    if (int st = scan_rows(w, ws, 0, 1, N, batch, f + batch, s); st != JW_OK) return st;
+  }
   for (int b0 = 0; b0 < batch; b0 += 65535) {
     const int nb = batch - b0 < 65535 ? batch - b0 : 65535;
     dim3 grid((unsigned)((N + kNT - 1) / kNT), (unsigned)nb);
     hipLaunchKernelGGL((modwt_inv_level<L, FMA>), grid, dim3(kNT), 0, s, v + b0 * vs, vs,
-                       w + b0 * ws, ws, out + b0 * os, os, N, 1L << (j - 1), t);
+                       w + b0 * ws, ws, out + b0 * os, os, N, 1L << (j - 1), t,
+                       f ? f + b0 : nullptr, f ? f + batch + b0 : nullptr, nullptr);
   }
   JW_HIP_TRY(hipGetLastError());
   return JW_OK;

@@ -80,6 +80,16 @@ __device__ __forceinline__ double madd(double acc, double f, double v) {
   }
 }
 
+// Non-finite detection for JWave's zero-tap semantics (jw_modwt_nf.hip): a kernel that writes
+// a final row (V_J forward, x inverse) ORs !isfinite over every value it computes there and, at
+// its end, sets the signal's flag.  A non-finite sample anywhere in the cascade reaches that
+// row at its own position (tap m = 0 of every level carries it, and a sum with a non-finite
+// term is non-finite), so a clear flag proves the zero taps the kernels skip were all finite.
+// Lanes store the constant 1 (vector stores; every writer writes the same value).
+__device__ __forceinline__ void nonfinite_flag(int* nf, bool bad) {
+  if (nf != nullptr && bad) nf[blockIdx.y] = 1;
+}
+
 template <int L, int J>
 struct Geo {
   static constexpr int H = (L - 1) * ((1 << J) - 1);  // total history samples
@@ -136,7 +146,7 @@ __device__ __forceinline__ void bstore2(rsrc_t r, int off, d2 v) {
 template <int L, int J, bool FMA, int NT, int SCP, bool ONE, class Fetch>
 __device__ __forceinline__ void fwd_step(double* lds, d2& cur, Fetch&& fetch, int a, int P,
                                          int seg_end, const rsrc_t (&rw)[ONE ? 1 : J + 1],
-                                         int n8, const Taps& taps) {
+                                         int n8, const Taps& taps, bool& nf) {
   constexpr int C = 2 * NT;
   using G = GeoF<L, J, C>;
   const int t = threadIdx.x;
@@ -183,6 +193,7 @@ __device__ __forceinline__ void fwd_step(double* lds, d2& cur, Fetch&& fetch, in
       *(d2*)&lds[G::cs(j + 1) + i] = d2{v0, v1};
     } else {
       bstore2<SCP>(rw[ONE ? 0 : J], roff(J), d2{v0, v1});
+      nf |= !__builtin_isfinite(v0) | !__builtin_isfinite(v1);  // see nonfinite_flag
     }
     __syncthreads();
   }
@@ -213,7 +224,7 @@ template <int L, int J, bool FMA, int NT, int SCP = 0, bool ONE = false>
 __global__ __launch_bounds__(NT) void modwt_fwd_fast(const double* __restrict__ x,
                                                      double* __restrict__ coeffs, long N,
                                                      long seg_len, long warm, long npairs,
-                                                     Taps taps) {
+                                                     Taps taps, int* __restrict__ nf = nullptr) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   constexpr int C = 2 * NT;
   using G = GeoF<L, J, C>;
@@ -257,12 +268,14 @@ __global__ __launch_bounds__(NT) void modwt_fwd_fast(const double* __restrict__ 
 #pragma unroll
   for (int k = 0; k < 2 * (J + 1); ++k) bstore(rx, kOOB - 8 * k, 0.0);  // distinct: not merged
   __syncthreads();
+  bool bad = false;
   for (int k = 0; k < (int)npairs; ++k) {
-    fwd_step<L, J, FMA, NT, SCP, ONE>(lds, A, fetch, a, P, seg_end, rw, n8, taps);
+    fwd_step<L, J, FMA, NT, SCP, ONE>(lds, A, fetch, a, P, seg_end, rw, n8, taps, bad);
     a += C;
-    fwd_step<L, J, FMA, NT, SCP, ONE>(lds, B, fetch, a, P, seg_end, rw, n8, taps);
+    fwd_step<L, J, FMA, NT, SCP, ONE>(lds, B, fetch, a, P, seg_end, rw, n8, taps, bad);
     a += C;
   }
+  nonfinite_flag(nf, bad);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -304,7 +317,8 @@ template <int L, int J, bool FMA, int C, int NT, int RF, bool TOPG, class Fetch,
 __device__ __forceinline__ void inv_step(d2* vw, double (&cur)[(C / NT) * (J + 1)],
                                          Fetch&& fetch, long a, long P, long seg_end,
                                          const rsrc_t& rx, const Taps& taps, int (&rb)[J + 1],
-                                         double (&tv)[(C / NT) * 2 * L], TapLoad&& load_taps) {
+                                         double (&tv)[(C / NT) * 2 * L], TapLoad&& load_taps,
+                                         bool& nf) {
   using G = GeoI<L, J, C, TOPG>;
   using Rg = Ring<L, J, C, RF>;
   constexpr int R = C / NT;
@@ -388,6 +402,7 @@ __device__ __forceinline__ void inv_step(d2* vw, double (&cur)[(C / NT) * (J + 1
       } else {
         const long pos = a + i;
         bstore(rx, (pos >= P && pos < seg_end) ? (int)(pos * 8) : kOOB, v);
+        nf |= !__builtin_isfinite(v);
       }
     }
     JW_INV_SYNC();
@@ -430,7 +445,8 @@ template <int L, int J, bool FMA, int C, int NT, int D, int RF, bool TOPG, int M
 __global__ __launch_bounds__(NT, MINW) void modwt_inv_fast(const double* __restrict__ coeffs,
                                                            double* __restrict__ x, long N,
                                                            long seg_len, long a_start,
-                                                           long npairs, Taps taps) {
+                                                           long npairs, Taps taps,
+                                                           int* __restrict__ nf = nullptr) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   using G = GeoI<L, J, C, TOPG>;
   constexpr int R = C / NT;
@@ -513,14 +529,16 @@ __global__ __launch_bounds__(NT, MINW) void modwt_inv_fast(const double* __restr
 #pragma unroll
   for (int j = 0; j <= J; ++j) rb[j] = 0;
   __syncthreads();
+  bool bad = false;
   for (long k = 0; k < npairs; ++k) {  // npairs counts groups of D steps
 #pragma unroll
     for (int q = 0; q < D; ++q) {
       inv_step<L, J, FMA, C, NT, RF, TOPG>((d2*)lds, S[q], fetch, a, P, seg_end, rx, taps, rb,
-                                           tv, load_taps);
+                                           tv, load_taps, bad);
       a -= C;
     }
   }
+  nonfinite_flag(nf, bad);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -566,21 +584,22 @@ inline long pick_seg(long N, int batch, long warm, int C = kC, long min_wgs = 81
 template <class K>
 int launch(K kern, size_t lds, long nseg, int batch, int nt, hipStream_t s, const double* in,
            long in_stride, double* out, long out_stride, long N, long seg, long p4, long npairs,
-           const Taps& t) {
+           const Taps& t, int* nf) {
   JW_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)lds));
   for (int b0 = 0; b0 < batch; b0 += 65535) {
     const int nb = batch - b0 < 65535 ? batch - b0 : 65535;
     hipLaunchKernelGGL(kern, dim3((unsigned)nseg, (unsigned)nb), dim3(nt), lds, s,
                        in + (long)b0 * in_stride, out + (long)b0 * out_stride, N, seg, p4, npairs,
-                       t);
+                       t, nf ? nf + b0 : nullptr);
   }
   JW_HIP_TRY(hipGetLastError());
   return JW_OK;
 }
 
 template <int L, int J, bool FMA>
-int launch_fwd(const Taps& t, const double* x, double* c, long N, int batch, hipStream_t s) {
+int launch_fwd(const Taps& t, const double* x, double* c, long N, int batch, hipStream_t s,
+               int* nf) {
   constexpr int NT = 256, C = 2 * NT;
   using G = GeoF<L, J, C>;
   const long warm = ((long)(G::H + C - 1) / C) * C;
@@ -592,13 +611,14 @@ int launch_fwd(const Taps& t, const double* x, double* c, long N, int batch, hip
   const char* g1 = knob("JW_FWD_ONE_RSRC");  // A/B runs: 0 = one resource per row
   if (cs * 8 < (long)kOOB && !(g1 && g1[0] == '0'))
     return launch(modwt_fwd_fast<L, J, FMA, NT, JW_FWD_SCP, true>, lds, nseg, batch, NT, s, x, N, c, cs, N,
-                  seg, warm, npairs, t);
+                  seg, warm, npairs, t, nf);
   return launch(modwt_fwd_fast<L, J, FMA, NT, JW_FWD_SCP>, lds, nseg, batch, NT, s, x, N, c, cs, N, seg, warm,
-                npairs, t);
+                npairs, t, nf);
 }
 
 template <int L, int J, bool FMA, int C, int NT, int D, int RF, bool TOPG = false>
-int launch_inv_c(const Taps& t, const double* c, double* x, long N, int batch, hipStream_t s) {
+int launch_inv_c(const Taps& t, const double* c, double* x, long N, int batch, hipStream_t s,
+                 int* nf) {
   using G = GeoI<L, J, C, TOPG>;
   const long warm = ((long)(G::H + C - 1) / C) * C;
   const long seg = pick_seg(N, batch, warm, C);
@@ -612,7 +632,7 @@ int launch_inv_c(const Taps& t, const double* c, double* x, long N, int batch, h
   constexpr int kFit = (int)((160 * 1024) / ((size_t)G::inv_total * sizeof(double)));
   constexpr int kMinW = (kFit < 1 ? 1 : kFit > 4 ? 4 : kFit) * NT / 256;
   return launch(modwt_inv_fast<L, J, FMA, C, NT, D, RF, TOPG, (kMinW < 1 ? 1 : kMinW)>, lds, nseg,
-                batch, NT, s, c, cs, x, N, N, seg, a_start, ngroups, t);
+                batch, NT, s, c, cs, x, N, N, seg, a_start, ngroups, t, nf);
 }
 
 template <int L, int J, int C>
@@ -634,7 +654,8 @@ namespace jw {
 namespace fast {
 
 template <int L, int J, bool FMA>
-int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hipStream_t s) {
+int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hipStream_t s,
+               int* nf) {
   // The barrier-free kernels are the default wherever they fit: two outputs per lane on the LDS
   // levels (wave2, N even: 16-byte pairs) where inv_prefer2 says so, else one (wave).
   // JW_INV_KERNEL = wave2 / wave / wg forces one of them (A/B runs and the parity tests).
@@ -645,10 +666,10 @@ int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hip
   if constexpr (wave2::inv_ok<L, J>()) {
     if ((N % 2) == 0 && (force_w2 || (!force_wg && !(force_w1 && wave::inv_wave_ok<L, J>()) &&
                      (wave2::inv_prefer2<L, J, FMA>() || !wave::inv_wave_ok<L, J>()))))
-      return wave2::launch_inv<L, J, FMA>(t, c, x, N, batch, s);
+      return wave2::launch_inv<L, J, FMA>(t, c, x, N, batch, s, nf);
   }
   if constexpr (wave::inv_wave_ok<L, J>()) {
-    if (!force_wg) return wave::launch_inv_wave<L, J, FMA>(t, c, x, N, batch, s);
+    if (!force_wg) return wave::launch_inv_wave<L, J, FMA>(t, c, x, N, batch, s, nf);
   }
   constexpr int RF = J >= 7 ? 7 : J + 1;
   const char* e = knob("JW_INV_RING");
@@ -657,14 +678,14 @@ int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hip
   const bool lds_top = !(top && top[0] == 'g');
   const bool c512 = ce && ce[0] == '5';
   if (e && e[0] == 'o') {
-    if (lds_top || J < 2) return launch_inv_c<L, J, FMA, 256, 256, 2, J + 1>(t, c, x, N, batch, s);
-    return launch_inv_c<L, J, FMA, 256, 256, 2, J + 1, (J >= 2)>(t, c, x, N, batch, s);
+    if (lds_top || J < 2) return launch_inv_c<L, J, FMA, 256, 256, 2, J + 1>(t, c, x, N, batch, s, nf);
+    return launch_inv_c<L, J, FMA, 256, 256, 2, J + 1, (J >= 2)>(t, c, x, N, batch, s, nf);
   }
-  if (lds_top || J < 2) return launch_inv_c<L, J, FMA, 256, 256, 2, RF>(t, c, x, N, batch, s);
+  if (lds_top || J < 2) return launch_inv_c<L, J, FMA, 256, 256, 2, RF>(t, c, x, N, batch, s, nf);
   if constexpr (inv_fits_topg<L, J, 512>()) {
-    if (c512) return launch_inv_c<L, J, FMA, 512, 256, 2, RF, true>(t, c, x, N, batch, s);
+    if (c512) return launch_inv_c<L, J, FMA, 512, 256, 2, RF, true>(t, c, x, N, batch, s, nf);
   }
-  return launch_inv_c<L, J, FMA, 256, 256, 2, RF, (J >= 2)>(t, c, x, N, batch, s);
+  return launch_inv_c<L, J, FMA, 256, 256, 2, RF, (J >= 2)>(t, c, x, N, batch, s, nf);
 }
 
 // Returned when (L, J, N) has no fast kernel (the caller falls back to the generic ones).
@@ -672,14 +693,14 @@ constexpr int kNotHandled = -100;
 
 template <int L>
 int forward(const Taps& t, bool fma, const double* x, double* c, long N, int J, int batch,
-            hipStream_t s) {
+            hipStream_t s, int* nf) {
   if (N < kC || (N & 1) || N >= (1L << 27)) return kNotHandled;
   int st = kNotHandled;
   auto one = [&](auto jc) {
     constexpr int JJ = decltype(jc)::value;
     if constexpr (fwd_ok<L, JJ>()) {
-      st = fma ? launch_fwd<L, JJ, true>(t, x, c, N, batch, s)
-               : launch_fwd<L, JJ, false>(t, x, c, N, batch, s);
+      st = fma ? launch_fwd<L, JJ, true>(t, x, c, N, batch, s, nf)
+               : launch_fwd<L, JJ, false>(t, x, c, N, batch, s, nf);
     }
   };
   switch (J) {
@@ -697,14 +718,14 @@ int forward(const Taps& t, bool fma, const double* x, double* c, long N, int J, 
 
 template <int L>
 int inverse(const Taps& t, bool fma, const double* c, double* x, long N, int J, int batch,
-            hipStream_t s) {
+            hipStream_t s, int* nf) {
   if (N < kC || N >= (1L << 27)) return kNotHandled;
   int st = kNotHandled;
   auto one = [&](auto jc) {
     constexpr int JJ = decltype(jc)::value;
     if constexpr (inv_ok<L, JJ>()) {
-      st = fma ? launch_inv<L, JJ, true>(t, c, x, N, batch, s)
-               : launch_inv<L, JJ, false>(t, c, x, N, batch, s);
+      st = fma ? launch_inv<L, JJ, true>(t, c, x, N, batch, s, nf)
+               : launch_inv<L, JJ, false>(t, c, x, N, batch, s, nf);
     }
   };
   switch (J) {
@@ -722,14 +743,14 @@ int inverse(const Taps& t, bool fma, const double* c, double* x, long N, int J, 
 
 #define JW_FAST_EXTERN(LL)                                                                     \
   extern template int forward<LL>(const Taps&, bool, const double*, double*, long, int, int,   \
-                                  hipStream_t);                                                \
+                                  hipStream_t, int*);                                          \
   extern template int inverse<LL>(const Taps&, bool, const double*, double*, long, int, int,   \
-                                  hipStream_t);
+                                  hipStream_t, int*);
 #define JW_FAST_INSTANTIATE(LL)                                                                \
   template int forward<LL>(const Taps&, bool, const double*, double*, long, int, int,          \
-                           hipStream_t);                                                       \
+                           hipStream_t, int*);                                                 \
   template int inverse<LL>(const Taps&, bool, const double*, double*, long, int, int,          \
-                           hipStream_t);
+                           hipStream_t, int*);
 #define JW_FAST_LENGTHS(X) X(2) X(4) X(6) X(8) X(12) X(16) X(20)
 
 JW_FAST_LENGTHS(JW_FAST_EXTERN)

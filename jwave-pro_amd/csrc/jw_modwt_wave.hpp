@@ -93,7 +93,8 @@ __device__ __forceinline__ void wave_lds_sync() {
 template <int L, int J, bool FMA, int D, int U, int MEM = 1, int CP = 0>
 __global__ __launch_bounds__(kW) void modwt_inv_wave(const double* __restrict__ coeffs,
                                                      double* __restrict__ x, long N, long seg_len,
-                                                     long a_start, long ngroups, Taps taps) {
+                                                     long a_start, long ngroups, Taps taps,
+                                                     int* __restrict__ nf = nullptr) {
   static_assert(U % D == 0, "U must be a multiple of D");
   using G = WGeo<L, J>;
   constexpr int JL = G::JL;
@@ -141,6 +142,7 @@ __global__ __launch_bounds__(kW) void modwt_inv_wave(const double* __restrict__ 
   }
   wave_lds_sync();
 
+  bool bad = false;
   for (int g = 0; g < (int)ngroups; ++g) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -208,9 +210,11 @@ __global__ __launch_bounds__(kW) void modwt_inv_wave(const double* __restrict__ 
       }
       const int pos = a + lane;
       bstore(rx, (MEM && pos >= P && pos < seg_end) ? pos * 8 : kOOB, v);
+      bad |= !__builtin_isfinite(v);
       a -= kW;
     }
   }
+  fast::nonfinite_flag(nf, bad);
 }
 
 template <int L, int J>
@@ -222,7 +226,7 @@ constexpr bool inv_wave_ok() {
 
 template <int L, int J, bool FMA>
 int launch_inv_wave(const Taps& t, const double* c, double* x, long N, int batch,
-                    hipStream_t s) {
+                    hipStream_t s, int* nf) {
   using G = WGeo<L, J>;
   constexpr int D = 3, U = 6;
   const long warm = ((long)(G::H + kW - 1) / kW) * kW;
@@ -240,7 +244,8 @@ int launch_inv_wave(const Taps& t, const double* c, double* x, long N, int batch
   for (int b0 = 0; b0 < batch; b0 += 65535) {
     const int nb = batch - b0 < 65535 ? batch - b0 : 65535;
     hipLaunchKernelGGL(kern, dim3((unsigned)nseg, (unsigned)nb), dim3(kW), lds, s,
-                       c + (long)b0 * cstride, x + (long)b0 * N, N, seg, a_start, ngroups, t);
+                       c + (long)b0 * cstride, x + (long)b0 * N, N, seg, a_start, ngroups, t,
+                       nf ? nf + b0 : nullptr);
   }
   JW_HIP_TRY(hipGetLastError());
   return JW_OK;

@@ -190,7 +190,8 @@ template <int L, int J, bool FMA, int D, int U, int MEM = 1, bool ONE = false,
           bool ROT = JW_INV2_ROT != 0>
 __global__ __launch_bounds__(64) void modwt_inv_wave2(const double* __restrict__ coeffs,
                                                       double* __restrict__ x, long N, long seg_len,
-                                                      long a_start, long ngroups, Taps taps) {
+                                                      long a_start, long ngroups, Taps taps,
+                                                      int* __restrict__ nf = nullptr) {
   static_assert(U % D == 0, "U must be a multiple of D");
   using G = G2<L, J>;
   using GW = typename G::W1;
@@ -266,6 +267,7 @@ __global__ __launch_bounds__(64) void modwt_inv_wave2(const double* __restrict__
   }
   wave_lds_sync();
 
+  bool bad = false;
   for (int gi = 0; gi < (int)ngroups; ++gi) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -329,9 +331,11 @@ __global__ __launch_bounds__(64) void modwt_inv_wave2(const double* __restrict__
       LdsLevels<L, J, FMA, JL>::run(lds, lane, taps, v, cur.w, hp);
       const int pos = a + 2 * lane;
       bstore2(rx, (MEM && pos >= P && pos < seg_end) ? (int)(pos * 8) : kOOB, d2{v[0], v[1]});
+      bad |= !__builtin_isfinite(v[0]) | !__builtin_isfinite(v[1]);
       a -= kS;
     }
   }
+  fast::nonfinite_flag(nf, bad);
 }
 
 template <int L, int J>
@@ -356,7 +360,8 @@ constexpr bool inv_prefer2() {
 // steps per loop trip: 2, or 4 for 16 taps with ROT (the level-6 rings of 8 entries then rotate
 // once per trip; at 8 taps they are 4 long and U = 2 suffices)
 template <int L, int J, bool FMA, int D = 2, int U = (JW_INV2_ROT && L == 16) ? 4 : 2>
-int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hipStream_t s) {
+int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hipStream_t s,
+               int* nf) {
   using G = G2<L, J>;
   const long warm = ((long)(G::H + kS - 1) / kS) * kS;
   const long seg = fast::pick_seg(N, batch, warm, kS, 8192);
@@ -375,7 +380,8 @@ int launch_inv(const Taps& t, const double* c, double* x, long N, int batch, hip
   for (int b0 = 0; b0 < batch; b0 += 65535) {
     const int nb = batch - b0 < 65535 ? batch - b0 : 65535;
     hipLaunchKernelGGL(kern, dim3((unsigned)nseg, (unsigned)nb), dim3(64), lds, s,
-                       c + (long)b0 * cstride, x + (long)b0 * N, N, seg, a_start, ngroups, t);
+                       c + (long)b0 * cstride, x + (long)b0 * N, N, seg, a_start, ngroups, t,
+                       nf ? nf + b0 : nullptr);
   }
   JW_HIP_TRY(hipGetLastError());
   return JW_OK;

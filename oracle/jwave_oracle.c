@@ -401,16 +401,17 @@ void jwo_modwt_inverse_fft(const double* coeffs, long N, int J, const double* g,
 }
 
 /* performConvolution with ConvolutionMethod.AUTO (:640-664): per call, FFT when the int32
- * product signal.length * filter.length exceeds fftConvolutionThreshold, else DIRECT (the
- * zero-skipping sums, bit-identical to circularConvolve for finite inputs). */
+ * product signal.length * filter.length exceeds fftConvolutionThreshold, else DIRECT: the
+ * faithful every-tap circularConvolve{,Adjoint}, so non-finite samples meet the zero taps as
+ * in the reference (0 * Inf = NaN). */
 static __thread int g_auto_threshold = 4096;
 static void auto_conv(const double* s, long N, const double* f, long M, int L, double* out) {
   if (jwo_modwt_auto_uses_fft(N, M, g_auto_threshold)) fft_conv(s, N, f, M, L, out);
-  else circ_conv_nz(s, N, f, M, L, out);
+  else circ_conv(s, N, f, M, L, out);
 }
 static void auto_conv_adj(const double* s, long N, const double* f, long M, int L, double* out) {
   if (jwo_modwt_auto_uses_fft(N, M, g_auto_threshold)) fft_conv_adj(s, N, f, M, L, out);
-  else circ_conv_adj_nz(s, N, f, M, L, out);
+  else circ_conv_adj(s, N, f, M, L, out);
 }
 void jwo_modwt_forward_auto(const double* x, long N, int J, const double* g, const double* h,
                             int L, int threshold, double* coeffs) {
