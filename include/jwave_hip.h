@@ -88,7 +88,9 @@ long jw_release_caches(void);
  * §9).  Each is read from the environment once, on first use; jw_set_knob(name, value)
  * replaces that value for later calls (value NULL = unset), so a test changes a setting without
  * setenv racing the engine's threads.  name must start with "JW_" (else
- * JW_ERR_ILLEGAL_ARGUMENT).  jw_get_knob returns the value in effect, or NULL when unset; the
+ * JW_ERR_ILLEGAL_ARGUMENT).  JW_PIN_MB, JW_PIN_RING and JW_COPY_THREADS size process-wide
+ * host staging on first use and are environment-only: jw_set_knob refuses them
+ * (JW_ERR_ILLEGAL_ARGUMENT).  jw_get_knob returns the value in effect, or NULL when unset; the
  * string stays valid for the life of the process. */
 int jw_set_knob(const char* name, const char* value);
 const char* jw_get_knob(const char* name);

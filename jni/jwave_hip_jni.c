@@ -366,6 +366,7 @@ static void aioobe(JNIEnv* env, jsize index, jsize length) {
  * spcTime[i][j][k]: a null slab or row throws NullPointerException, one shorter than the box
  * ArrayIndexOutOfBoundsException, and anything past the box is ignored.  0 = exception pending. */
 static int slab_in(JNIEnv* env, jobjectArray m, jsize d2, jsize d3, double* dst) {
+  if (d2 == 0 || d3 == 0) return 1;  /* the copy loops never index spcTime[i]: nothing to read */
   if (!m) {
     npe(env);
     return 0;
@@ -445,6 +446,20 @@ JNIEXPORT jobjectArray JNICALL Java_jwave_hip_HipFastWaveletTransform_nSpace(
     if (!ok) {
       free(x);
       return NULL;
+    }
+    if (i == 0) {
+      /* the reference runs slab 0's 2-D transform (:530 / :623), which checks lvlP and lvlQ,
+       * before it reads slab 1: a level error wins over a malformed later slab.  batch 0 =
+       * the 2-D entry's checks only, in its order (the 3-D entry's for those two levels). */
+      const jw_fwt_plan* p0 = (const jw_fwt_plan*)(intptr_t)plan;
+      const int lv = op == 0
+                         ? jw_fwt2d_forward(p0, NULL, NULL, d2, d3, lvlP, lvlQ, 0, JW_HOST, NULL)
+                         : jw_fwt2d_reverse(p0, NULL, NULL, d2, d3, lvlP, lvlQ, 0, JW_HOST, NULL);
+      if (lv != JW_OK) {
+        free(x);
+        jw_throw(env, lv);
+        return NULL;
+      }
     }
   }
   double* y = malloc(sizeof(double) * (size_t)d1 * (slab ? slab : 1));

@@ -530,6 +530,13 @@ int jw_set_knob(const char* name, const char* value) {
   clear_error();
   if (!name || std::strncmp(name, "JW_", 3) != 0)
     return fail(JW_ERR_ILLEGAL_ARGUMENT, "setting name must start with JW_");
+  // sized once per process (the pinned bounce buffers and the copy-thread pool are built on
+  // first use): a later replacement could not take effect, so it is refused, not ignored
+  for (const char* fixed : {"JW_PIN_MB", "JW_PIN_RING", "JW_COPY_THREADS"})
+    if (std::strcmp(name, fixed) == 0)
+      return fail(JW_ERR_ILLEGAL_ARGUMENT,
+                  "%s is fixed at first use; set it in the environment before the first call",
+                  name);
   (void)knob(name);  // the environment's value first, so it is not read later over this one
   std::lock_guard<std::mutex> lk(g_knob_mu);
   knobs()[name] = value ? new std::string(value) : nullptr;  // the old value stays allocated

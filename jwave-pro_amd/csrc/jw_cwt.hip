@@ -812,12 +812,16 @@ static int side_stream(SideStream** out) {
   return JW_OK;
 }
 // Destroyed before the StreamAllocs declared ahead of it: the caller's stream waits for the side
-// stream's work before the buffers that work reads are freed.
+// stream's work before the buffers that work reads are freed.  The join event is recorded here,
+// at scope exit, behind everything the call queued on the side stream, so an early error return
+// after some side launches joins them too (no stale or never-recorded event).
 struct JoinGuard {
   hipStream_t s = nullptr;
   SideStream* side = nullptr;
   ~JoinGuard() {
-    if (side) (void)hipStreamWaitEvent(s, side->join, 0);
+    if (!side) return;
+    (void)hipEventRecord(side->join, side->s);
+    (void)hipStreamWaitEvent(s, side->join, 0);
   }
 };
 
@@ -1183,7 +1187,12 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     const bool use_par = !(gpr && gpr[0] == '0');
     const bool nt = (ntm & 2) != 0;
     long woff = 0, roff = 0;
+    // JW_TEST_CWT_FAIL_GROUP=k (tests only): fail at coarse group k, after groups < k have
+    // launched on the side stream -- the error path must still join them (JoinGuard)
+    const char* gtf = knob("JW_TEST_CWT_FAIL_GROUP");
+    const long fail_group = gtf ? std::atol(gtf) : -1;
     for (size_t g = 0; g < groups.size() && st == JW_OK; ++g) {
+      if ((long)g == fail_group) return fail(JW_ERR_FAILURE, "CWT: injected failure at coarse group %ld", (long)g);
       const CoarseGroup& G = groups[g];
       const long M = G.M, N1c = M / 512, P = N / M;
       const Tables& TM = gT[g];
@@ -1244,7 +1253,6 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
       }
     }
   }
-  if (join.side) JW_HIP_TRY(hipEventRecord(join.side->join, bs));
   // the other (signal, scale) pairs: IFFT(X * psi_hat) -> coefficients in two passes
   if (pipe && st == JW_OK) {
     auto go = [&](auto kind) {

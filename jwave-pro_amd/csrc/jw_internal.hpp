@@ -145,7 +145,13 @@ template <class Key, class Fill>
 int cached_table(DevCache<Key>& cache, const Key& key, size_t bytes, StreamAllocs& mem,
                  hipStream_t s, const void** out, Fill&& fill) {
   if ((*out = cache.find(key)) != nullptr) return JW_OK;
-  if (!cache.fits(bytes)) {
+  // A table is kept for the process only while it fits the cache's budget AND a quarter of the
+  // device memory that is free right now, so a co-resident framework that holds most of HBM is
+  // not starved by tables the engine would keep after the call.
+  size_t free_b = 0, total_b = 0;
+  const bool roomy = hipMemGetInfo(&free_b, &total_b) == hipSuccess && bytes <= free_b / 4;
+  if (!roomy) (void)hipGetLastError();
+  if (!roomy || !cache.fits(bytes)) {
     void* p = nullptr;
     JW_HIP_TRY(mem.alloc(&p, bytes));
     *out = p;

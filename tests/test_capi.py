@@ -51,6 +51,10 @@ def test_knobs_read_once_and_overridable(knobs):
     assert _native.get_knob("JW_TEST_KNOB_NEVER_SET") is None
     with pytest.raises(IllegalArgumentException, match="JW_"):
         _native.set_knob("OMP_NUM_THREADS", "1")
+    # host-staging sizes are fixed at first use: refused, never silently ignored
+    for fixed in ("JW_PIN_MB", "JW_PIN_RING", "JW_COPY_THREADS"):
+        with pytest.raises(IllegalArgumentException, match="fixed at first use"):
+            _native.set_knob(fixed, "4")
 
 
 def test_jni_glue_binds_only_exported_symbols():

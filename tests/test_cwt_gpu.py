@@ -377,3 +377,25 @@ def test_cfg3_full_scale_set():
         assert nw(got[b], jw) < TOL_JWAVE, nw(got[b], jw)
         for i in range(64):
             assert nw(got[b, i], ex[i]) < 1e-11, (b, i, nw(got[b, i], ex[i]))
+
+
+def test_error_after_side_stream_launches_joins(knobs):
+    # an error return after some coarse-grid groups have launched on the side stream
+    # must still join them before the call's buffers are freed.  JW_TEST_CWT_FAIL_GROUP=1 fails
+    # at the second group (groups 0 launched); the call raises, then the same call without the
+    # injection equals the one made before it, bit for bit, with the side stream forced on.
+    from jwave.exceptions import JWaveFailure
+    knobs.setenv("JW_CWT_OVERLAP", "1")
+    n = 1 << 16
+    scales = CWT.generateLogScales(2.0, 1024.0, 24)
+    x = orc.fill_uniform(n, 31)
+    t = CWT(MorletWavelet(*MORLET6))
+    before = t.transformFFT(x, scales, 1.0).getCoefficients()
+    knobs.setenv("JW_TEST_CWT_FAIL_GROUP", "1")
+    for _ in range(3):
+        with pytest.raises(JWaveFailure, match="injected failure"):
+            t.transformFFT(x, scales, 1.0)
+    knobs.delenv("JW_TEST_CWT_FAIL_GROUP")
+    import torch
+    torch.cuda.synchronize()
+    assert np.array_equal(t.transformFFT(x, scales, 1.0).getCoefficients(), before)

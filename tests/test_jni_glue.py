@@ -176,6 +176,23 @@ def test_fwt_space_malformed_throws_what_the_reference_throws(jni):
             jni.L.mock_oset(o, 0, jni.matrix(np.ones((4, 8))))
             jni.call("HipFastWaveletTransform_nSpace", p, op, o, 1, 1, 1)
         assert e.value.cls == NPE
+        # invalid lvlP / lvlQ with a null (or short) later slab: the reference's slab-0 2-D
+        # transform throws first (BasicTransform.java:530 / :623), before slab 1 is read
+        for bad in (None, np.ones((4, 4))):
+            with pytest.raises(JavaException) as e:
+                o = jni.L.mock_oarray(2, b"[[D")
+                jni.L.mock_oset(o, 0, jni.matrix(np.ones((4, 8))))
+                if bad is not None:
+                    jni.L.mock_oset(o, 1, jni.matrix(bad))
+                jni.call("HipFastWaveletTransform_nSpace", p, op, o, 3, 1, 1)
+            assert e.value.cls == FAILURE and "out of range" in e.value.msg
+        # invalid lvlR only: reported after every slab was read (the 1-D pass comes last), so
+        # the malformed slab's exception wins
+        with pytest.raises(JavaException) as e:
+            o = jni.L.mock_oarray(2, b"[[D")
+            jni.L.mock_oset(o, 0, jni.matrix(np.ones((4, 8))))
+            jni.call("HipFastWaveletTransform_nSpace", p, op, o, 1, 1, 5)
+        assert e.value.cls == NPE
     jni.call("HipFastWaveletTransform_nPlanDestroy", p)
 
 
