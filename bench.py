@@ -218,6 +218,12 @@ def main_cwt(args, dev, rank, world):
         lib.jw_synth_uniform(ctypes.c_void_p(x.data_ptr()), n, B, 7 + rank * B, sptr)))
     prm = (ctypes.c_double * 2)(fb, fc)
     sc = np.ascontiguousarray(scales)
+    # the engine's own scale split for this call (jw_cwt_fft_paths: the rule jw_cwt_fft runs)
+    split = [ctypes.c_int(0) for _ in range(3)]
+    _native.check(lib.jw_cwt_fft_paths(_native.JW_CWT_MORLET, prm, n,
+                                       sc.ctypes.data_as(ctypes.c_void_p), ns, 1.0,
+                                       *[ctypes.byref(v) for v in split]))
+    n_two, n_band, n_coarse = (v.value for v in split)
 
     def call():
         _native.check(lib.jw_cwt_fft(_native.JW_CWT_MORLET, prm, ctypes.c_void_p(x.data_ptr()), n,
@@ -289,11 +295,14 @@ def main_cwt(args, dev, rank, world):
                          "note": "one launch = one jw_cwt_fft call over the batch (all FFT "
                                  "passes); traffic = rocprofv3 FETCH_SIZE*2 + WRITE_SIZE per call "
                                  f"({os.path.relpath(TRAFFIC_STEP_FILE, ROOT)}): the A workspace round "
-                                 "trip of the 27 two-pass scales (a < 29) is the excess over "
-                                 "algorithmic; the 37 scales whose band fits a coarse grid of "
-                                 "N/P points (P >= 4) run as an M-point inverse DFT (cwt_band512 "
-                                 "on the coarse grid) plus a Kaiser-Bessel interpolation "
-                                 "(cwt_interp) that writes each coefficient once (DESIGN.md 5.4)"},
+                                 f"trip of the {n_two} two-pass scales is the excess over "
+                                 f"algorithmic; the {n_coarse} scales whose band fits a coarse grid "
+                                 "of N/P points (P >= 4) run as an M-point inverse DFT "
+                                 "(cwt_band512 on the coarse grid) plus a Kaiser-Bessel "
+                                 "interpolation (cwt_interp) that writes each coefficient once, "
+                                 f"and {n_band} through the one-pass band kernel (DESIGN.md 5.4; "
+                                 "split from jw_cwt_fft_paths)",
+                         "scale_split": {"two_pass": n_two, "band": n_band, "coarse_grid": n_coarse}},
             "cpu_baseline": cpu}), flush=True)
 
 

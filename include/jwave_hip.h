@@ -238,6 +238,13 @@ int jw_fwt3d_reverse(const jw_fwt_plan* plan, const double* y, double* x, int d1
 int jw_cwt_fft(int wavelet, const double* params, const double* x, long n, const double* scales,
                int ns, double sampling_rate, int padding, double* out_reim, int batch, int where,
                void* stream);
+/* How jw_cwt_fft splits a call's scales (no device work, no data): *two_pass scales through
+ * the two-pass FFT, *band through the one-pass band kernel, *coarse_grid through the coarse
+ * grid + Kaiser-Bessel interpolation, under the engine's current settings
+ * (jw_set_knob JW_CWT_BAND / JW_CWT_INTERP).  For measurement tools and tests; the counts
+ * sum to ns.  Argument checks as jw_cwt_fft. */
+int jw_cwt_fft_paths(int wavelet, const double* params, long n, const double* scales, int ns,
+                     double sampling_rate, int* two_pass, int* band, int* coarse_grid);
 /* ContinuousWaveletTransform.transform(signal, scales, fs) -- the direct time-domain CWT
  * (:153-172, computeCoefficient :240-260; transformParallel :470-500 and
  * transformParallelCustom :577-680 give the same values).  Same wavelet kinds and parameter

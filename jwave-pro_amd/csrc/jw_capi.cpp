@@ -1044,6 +1044,16 @@ int jw_cwt_fft(int wavelet, const double* params, const double* x, long n, const
                    });
 }
 
+int jw_cwt_fft_paths(int wavelet, const double* params, long n, const double* scales, int ns,
+                     double sampling_rate, int* two_pass, int* band, int* coarse_grid) {
+  clear_error();
+  int st = cwt_fft_check(wavelet, params, n, scales, ns, JW_PAD_ZERO, 0, JW_HOST);
+  if (st != JW_OK) return st;
+  if (!two_pass || !band || !coarse_grid)
+    return fail(JW_ERR_ILLEGAL_ARGUMENT, "output pointer is null");
+  return cwt_fft_paths(wavelet, params, n, scales, ns, sampling_rate, two_pass, band, coarse_grid);
+}
+
 // transformFFT(...).getScalogram() with the coefficients kept in a device workspace (signals
 // in chunks of at most ~2 GiB of coefficients): only batch x ns energies leave the GPU.
 int jw_cwt_fft_scalogram(int wavelet, const double* params, const double* x, long n,

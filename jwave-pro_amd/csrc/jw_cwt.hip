@@ -907,22 +907,20 @@ static void interp_weights(long P, long N, std::vector<double>& wt) {
     }
 }
 
-// Group sizes: signals per forward chunk and (signal, scale) pairs per inverse group, so the
-// workspace A stays ~96 MB at N = 2^18 (two of them when pipelined).
-int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
-                   const double* scales_host, int ns, double fs, int padding, double* out,
-                   int batch, hipStream_t s) {
-  if (n == 0 || ns == 0 || batch == 0) return JW_OK;
-  long N = 1;
-  while (N < n) N <<= 1;  // MathUtils.nextPowerOfTwo :46-49
-  // 2^25 and 2^26 run the generic four-step passes (8192-point lines in 128 KB of LDS)
-  if (N > (1L << 26)) return fail(JW_ERR_UNSUPPORTED, "CWT padded length %ld > 2^26", N);
-  if ((long)batch * ns >= (1L << 31))
-    return fail(JW_ERR_UNSUPPORTED, "CWT batch x scales = %ld >= 2^31", (long)batch * ns);
-  Tables T;
-  int st = fft::tables(N, &T);
-  if (st != JW_OK) return st;
+// Which path each scale of a jw_cwt_fft call takes (band kernel, coarse grid, two-pass), with
+// the wavelet's spectrum parameters: the rule cwt_fft_device runs and jw_cwt_fft_paths reports.
+struct CwtSplit {
   WaveletFT w{};
+  std::vector<BandScale> bands, coarse;  // coarse sorted by M, grouped in groups
+  std::vector<int> full;                 // two-pass scales
+  std::vector<CoarseGroup> groups;
+  long psi_total = 0;
+  int nb_hi = 0;
+};
+static void cwt_split(int wavelet, const double* params, long N, const double* scales_host, int ns,
+                      double fs, CwtSplit* sp) {
+  WaveletFT& w = sp->w;
+  w = WaveletFT{};
   w.kind = wavelet;
   if (wavelet == JW_CWT_MORLET) {
     w.p0 = params[0];
@@ -946,8 +944,6 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   } else {
     w.norm = std::sqrt(2.0 * kPi);  // MeyerWavelet.java:244
   }
-  const char* gnt = knob("JW_CWT_NT");  // A/B runs: bit 1 = NT stores of A, 2 = of coeffs
-  const int ntm = gnt ? std::atoi(gnt) : 2;  // measured best: NT coefficient stores only
   w.p2 = wavelet == JW_CWT_MORLET ? -2.0 * kPi * kPi * w.p0 : -0.5 * w.p0 * w.p0;
   // Scales whose band spans at most nbmax 512-bin blocks run in one pass (cwt_band512); the
   // rest through the two-pass FFT.  One pass costs ~1.1 us per (signal, scale) pair at N = 2^18
@@ -960,11 +956,12 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   const char* gip = knob("JW_CWT_INTERP");
   const long pmin = gip ? std::atol(gip) : 4;
   const long N1b = N / 512;
-  std::vector<BandScale> bands, coarse;  // coarse: sorted by M below
+  auto& bands = sp->bands;
+  auto& coarse = sp->coarse;  // sorted by M below
   std::vector<long> coarse_m;
-  std::vector<int> full;
-  long psi_total = 0;
-  int nb_hi = 0;
+  auto& full = sp->full;
+  long& psi_total = sp->psi_total;
+  int& nb_hi = sp->nb_hi;
   for (int i = 0; i < ns; ++i) {
     long b0 = 0;
     int nb = 0;
@@ -988,7 +985,7 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     }
   }
   // coarse scales grouped by M (one band-kernel and one interpolation launch per group)
-  std::vector<CoarseGroup> groups;
+  auto& groups = sp->groups;
   {
     std::vector<int> ord(coarse.size());
     for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
@@ -1006,6 +1003,35 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     }
     coarse = std::move(sorted);
   }
+}
+
+// Group sizes: signals per forward chunk and (signal, scale) pairs per inverse group, so the
+// workspace A stays ~96 MB at N = 2^18 (two of them when pipelined).
+int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
+                   const double* scales_host, int ns, double fs, int padding, double* out,
+                   int batch, hipStream_t s) {
+  if (n == 0 || ns == 0 || batch == 0) return JW_OK;
+  long N = 1;
+  while (N < n) N <<= 1;  // MathUtils.nextPowerOfTwo :46-49
+  // 2^25 and 2^26 run the generic four-step passes (8192-point lines in 128 KB of LDS)
+  if (N > (1L << 26)) return fail(JW_ERR_UNSUPPORTED, "CWT padded length %ld > 2^26", N);
+  if ((long)batch * ns >= (1L << 31))
+    return fail(JW_ERR_UNSUPPORTED, "CWT batch x scales = %ld >= 2^31", (long)batch * ns);
+  Tables T;
+  int st = fft::tables(N, &T);
+  if (st != JW_OK) return st;
+  CwtSplit sp;
+  cwt_split(wavelet, params, N, scales_host, ns, fs, &sp);
+  const WaveletFT& w = sp.w;
+  const auto& bands = sp.bands;
+  const auto& coarse = sp.coarse;
+  const auto& full = sp.full;
+  const auto& groups = sp.groups;
+  const long psi_total = sp.psi_total;
+  const int nb_hi = sp.nb_hi;
+  const long N1b = N / 512;
+  const char* gnt = knob("JW_CWT_NT");  // A/B runs: bit 1 = NT stores of A, 2 = of coeffs
+  const int ntm = gnt ? std::atoi(gnt) : 2;  // measured best: NT coefficient stores only
   const int nband = (int)bands.size(), nfull = (int)full.size();
   const char* gmb = knob("JW_CWT_GROUP_MB");  // A/B runs: workspace size in MiB
   const long ws = (gmb ? std::atol(gmb) : 96L) << 20;  // 96 MB: profiles/r05/ab/cwt_group_p.txt
@@ -1292,6 +1318,18 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     }
   }
   return st;
+}
+
+int cwt_fft_paths(int wavelet, const double* params, long n, const double* scales, int ns,
+                  double fs, int* two_pass, int* band, int* coarse_grid) {
+  long N = 1;
+  while (N < n) N <<= 1;
+  CwtSplit sp;
+  if (n > 0 && ns > 0) cwt_split(wavelet, params, N, scales, ns, fs, &sp);
+  *two_pass = n > 0 ? (int)sp.full.size() : 0;
+  *band = (int)sp.bands.size();
+  *coarse_grid = (int)sp.coarse.size();
+  return JW_OK;
 }
 
 }  // namespace jw

@@ -243,6 +243,8 @@ int fft_device(int S, const double* in, double* out, long n, long batch, hipStre
 int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
                    const double* scales_host, int ns, double fs, int padding, double* out,
                    int batch, hipStream_t s);
+int cwt_fft_paths(int wavelet, const double* params, long n, const double* scales, int ns,
+                  double fs, int* two_pass, int* band, int* coarse_grid);
 int cwt_magnitude_device(const double* c, long count, double* out, hipStream_t s);
 int cwt_phase_device(const double* c, long count, double* out, hipStream_t s);
 int cwt_scalogram_device(const double* c, long rows, long n, double* energy, hipStream_t s);

@@ -52,7 +52,7 @@ EXPORTS = (
     "jw_fwt2d_forward", "jw_fwt2d_reverse", "jw_fwt3d_forward", "jw_fwt3d_reverse",
     "jw_synth_uniform", "jw_cwt_fft", "jw_cwt_direct", "jw_wpt_forward", "jw_wpt_reverse",
     "jw_fft_forward", "jw_fft_reverse", "jw_fft_forward_ex", "jw_fft_reverse_ex", "jw_cwt_magnitude", "jw_cwt_phase", "jw_cwt_scalogram",
-    "jw_cwt_fft_scalogram",
+    "jw_cwt_fft_scalogram", "jw_cwt_fft_paths",
 )
 
 _lib = None
@@ -119,6 +119,8 @@ def lib():
     L.jw_cwt_scalogram.argtypes = [c_dp, l, l, c_dp, i, c_dp]
     L.jw_cwt_fft_scalogram.argtypes = [i, c_dp, c_dp, l, c_dp, i, ctypes.c_double, i, c_dp, i, i,
                                        c_dp]
+    c_ip = ctypes.POINTER(ctypes.c_int)
+    L.jw_cwt_fft_paths.argtypes = [i, c_dp, l, c_dp, i, ctypes.c_double, c_ip, c_ip, c_ip]
     non_int = ("jw_last_error", "jw_version", "jw_modwt_plan_destroy", "jw_fwt_plan_destroy",
                "jw_release_caches", "jw_get_knob")
     for name in EXPORTS:

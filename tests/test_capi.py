@@ -444,3 +444,33 @@ def test_strict_range_contains_the_pyramid_range():
     (pyr_max,) = lim[_native.JW_ARITH_FMA]
     assert (pow2_max, other_max, pyr_max) == (1 << 28, 1 << 27, 1 << 23)
     assert pyr_max <= other_max <= pow2_max
+
+
+def test_cwt_fft_paths_reports_the_split(knobs):
+    # jw_cwt_fft_paths: the scale split jw_cwt_fft takes (host rule, no device work).  cfg3
+    # (Morlet omega0 = 6, 64 log scales 2..1024, N = 2^18): 22 two-pass scales and 42 on coarse
+    # grids; without coarse grids the band scales go to the band kernel
+    import ctypes
+    import math
+    from jwave import ContinuousWaveletTransform as CWT
+    lib = _native.lib()
+    scales = np.ascontiguousarray(CWT.generateLogScales(2.0, 1024.0, 64), dtype=np.float64)
+    params = (ctypes.c_double * 2)(1.0, 6.0 / (2 * math.pi))
+    out = [ctypes.c_int(-1) for _ in range(3)]
+
+    def split(n):
+        _native.check(lib.jw_cwt_fft_paths(_native.JW_CWT_MORLET, params, n,
+                                           scales.ctypes.data_as(ctypes.c_void_p), 64, 1.0,
+                                           *[ctypes.byref(o) for o in out]))
+        return tuple(o.value for o in out)
+
+    assert split(1 << 18) == (22, 0, 42)
+    knobs.setenv("JW_CWT_INTERP", "0")
+    t, b, c = split(1 << 18)
+    assert c == 0 and t + b == 64 and b > 0
+    knobs.setenv("JW_CWT_BAND", "0")
+    assert split(1 << 18) == (64, 0, 0)
+    assert split(1000) == (64, 0, 0)  # N = 1024 < 8192: no band paths at all
+    with pytest.raises(IllegalArgumentException):
+        _native.check(lib.jw_cwt_fft_paths(_native.JW_CWT_MORLET, params, -1, None, 64, 1.0,
+                                           *[ctypes.byref(o) for o in out]))
