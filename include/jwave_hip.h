@@ -230,7 +230,7 @@ int jw_fwt3d_reverse(const jw_fwt_plan* plan, const double* y, double* x, int d1
 /* coeffs[b][s][t] = IFFT(FFT(pad(x_b)) * conj(psi_hat(omega, scales[s], 0)))[t], t < n,
  * for batch signals x (batch x n); out_reim: batch x ns x n complex, interleaved (re, im).
  * scales: host array of ns positive scales (read at call time).  The padded length is
- * nextPowerOfTwo(n) <= 2^26.  Parameter checks follow the Java constructors:
+ * nextPowerOfTwo(n) <= 2^28 (past 2^26 in three passes; longer is JW_ERR_UNSUPPORTED).  Parameter checks follow the Java constructors:
  * fb, fc, sigma > 0 ("Bandwidth parameter must be positive", ...), Paul m and DOG n in range
  * ("Order parameter m must be a positive integer", ...), scales > 0 ("Scale must be positive";
  * not for Paul, whose fourierTransform(omega, scale, b) override :152-164 does not check).

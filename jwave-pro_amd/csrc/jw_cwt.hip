@@ -966,7 +966,9 @@ static void cwt_split(int wavelet, const double* params, long N, const double* s
     long b0 = 0;
     int nb = 0;
     double lo = 0.0, hi = 0.0;
-    const bool bandok = N >= 8192 && cwt_band(wavelet, w, scales_host[i], fs, N, &b0, &nb, &lo, &hi) &&
+    // (band and coarse-grid paths up to 2^26; the three-pass lengths run every scale two-pass)
+    const bool bandok = N >= 8192 && N <= (1L << 26) &&
+                        cwt_band(wavelet, w, scales_host[i], fs, N, &b0, &nb, &lo, &hi) &&
                         nb <= N1b;
     if (bandok && pmin > 0) {
       long M = 0, kc = 0, cb0 = 0;
@@ -1013,8 +1015,11 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   if (n == 0 || ns == 0 || batch == 0) return JW_OK;
   long N = 1;
   while (N < n) N <<= 1;  // MathUtils.nextPowerOfTwo :46-49
-  // 2^25 and 2^26 run the generic four-step passes (8192-point lines in 128 KB of LDS)
-  if (N > (1L << 26)) return fail(JW_ERR_UNSUPPORTED, "CWT padded length %ld > 2^26", N);
+  // 2^25 and 2^26 run the generic four-step passes (8192-point lines in 128 KB of LDS), 2^27
+  // and 2^28 three passes (fft::run_fft: the 16384 / 32768-point rows as FFTs of their own,
+  // through a second workspace), every scale two-pass
+  if (N > (1L << 28)) return fail(JW_ERR_UNSUPPORTED, "CWT padded length %ld > 2^28", N);
+  const bool three = N > (1L << 26);
   if ((long)batch * ns >= (1L << 31))
     return fail(JW_ERR_UNSUPPORTED, "CWT batch x scales = %ld >= 2^31", (long)batch * ns);
   Tables T;
@@ -1059,6 +1064,8 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   const long a_items = std::max(gsig, pipe ? 2 * gpair : gpair);
   JW_HIP_TRY(mem.alloc(&X, (size_t)batch * N * sizeof(cplx)));
   JW_HIP_TRY(mem.alloc(&A, (size_t)a_items * N * sizeof(cplx)));
+  cplx* Bw = nullptr;  // the three-pass lengths' second workspace (fft::run_fft)
+  if (three) JW_HIP_TRY(mem.alloc(&Bw, (size_t)a_items * N * sizeof(cplx)));
   // device scale table: [a_0 .. a_{ns-1} | (step, norm*sqrt(a)) per scale | (lo, hi) per scale]
   // (ScaleIn); (lo, hi) = the e^-60 band in signed bins, or the whole spectrum
   std::vector<double> hsc(5 * (size_t)ns);
@@ -1133,9 +1140,10 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     PadIn in{x + b0 * n, n, N / N1n, padding};
     const SpecOut so{X, N, N1n, N1, N / N1, b0};
     if (Xn) {
-      st = run_fft<-1>(N, nb, in, SpecOut1{X, N, b0}, SpecOutBoth{so, Xn}, A, s, T, (ntm & 1) != 0);
+      st = run_fft<-1>(N, nb, in, SpecOut1{X, N, b0}, SpecOutBoth{so, Xn}, A, s, T, (ntm & 1) != 0,
+                       true, Bw);
     } else {
-      st = run_fft<-1>(N, nb, in, SpecOut1{X, N, b0}, so, A, s, T, (ntm & 1) != 0);
+      st = run_fft<-1>(N, nb, in, SpecOut1{X, N, b0}, so, A, s, T, (ntm & 1) != 0, true, Bw);
     }
   }
   // with two-pass pairs to follow, the band kernel (FP64-issue bound) runs on a side stream
@@ -1307,7 +1315,7 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     auto go = [&](auto kind) {
       ScaleIn<decltype(kind)::value> in{X, dsc, w, N, N1, N <= 4096 ? 1 : N / N1, p0, pmf, fs,
                                         dsc + ns, dsc + 3 * ns, early};
-      return run_fft<1>(N, np_, in, o1, o, A, s, T, (ntm & 1) != 0);
+      return run_fft<1>(N, np_, in, o1, o, A, s, T, (ntm & 1) != 0, true, Bw);
     };
     switch (wavelet) {
       case JW_CWT_MORLET: st = go(std::integral_constant<int, JW_CWT_MORLET>{}); break;

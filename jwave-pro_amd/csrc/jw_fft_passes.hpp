@@ -1,6 +1,7 @@
 // jw_fft_passes.hpp -- the two FFT pass kernels and the four-step driver, shared by the
 // CWT (jw_cwt.hip) and MODWT FFT-convolution (jw_modwt_fft.hip) paths.  See jw_fft.hpp.
 #pragma once
+#include <algorithm>
 #include <type_traits>
 
 #include "jw_fft.hpp"
@@ -463,9 +464,41 @@ int run_fft_long(long N, long items, In1 in1, Out2 out_final, cplx* A, hipStream
   return JW_OK;
 }
 
-template <int S, class In1, class Out1, class Out2>
+// Three passes (N = 2^27, 2^28): pass 1 runs 8192-point columns as usual; the rows of N2 =
+// N / 8192 > 8192 points (too long for one workgroup's LDS) are then FFTs of their own, run as a
+// two-pass four-step (run_fft again, N2 = N1' x N2') over the items x 8192 rows, through a
+// second workspace B of the same size as A.
+constexpr int kMaxLog1 = 13;  // the longest pass-1 line: 8192 points in 128 KB of LDS
+// The four-step split used for length N: N1 = N (one pass) for N <= 4096, else
+// N1 = 2^min(ceil(log2 N / 2), 13), N2 = N / N1 (run_fft with long_ok = false).
+inline long split_n1(long N) {
+  if (N <= 4096) return N;
+  int logN = 0;
+  while ((1L << logN) < N) ++logN;
+  return 1L << std::min((logN + 1) / 2, kMaxLog1);
+}
+struct NestIn {  // row n1 of pass 1's workspace A as a line of N2 points, element N2i k1 + col
+  static constexpr bool kStrided = false;
+  const cplx* A;
+  long N, N1, N2, N2i;
+  __device__ cplx operator()(long item, long k1, long col) const {
+    const long it = item / N1, n1 = item - it * N1;
+    return A[it * N + n1 * N2 + N2i * k1 + col];
+  }
+};
+template <class Out>
+struct NestOut {  // the row FFT's output m = line + N1i idx is the outer n2 of row n1
+  Out out;
+  long N1, N1i, it0;
+  __device__ void operator()(long item, long idx, long line, cplx v) const {
+    const long it = item / N1, n1 = item - it * N1;
+    out(it0 + it, line + N1i * idx, n1, v);
+  }
+};
+
+template <int S, class In1, class Out1, class Out2, bool NEST = true>
 int run_fft(long N, long items, In1 in1, Out1 out_single, Out2 out_final, cplx* A, hipStream_t s,
-            const Tables& T, bool a_nt, bool long_ok = true) {
+            const Tables& T, bool a_nt, bool long_ok = true, cplx* B = nullptr) {
   int logN = 0;
   while ((1L << logN) < N) ++logN;
   if (long_ok && long_split(N)) return run_fft_long<S>(N, items, in1, out_final, A, s, T, a_nt);
@@ -475,9 +508,10 @@ int run_fft(long N, long items, In1 in1, Out1 out_single, Out2 out_final, cplx* 
     JW_HIP_TRY(hipGetLastError());
     return JW_OK;
   }
-  const int log1 = (logN + 1) / 2, log2 = logN - log1;
+  const int log1 = std::min((logN + 1) / 2, kMaxLog1), log2 = logN - log1;
   const long N1 = 1L << log1, N2 = 1L << log2;
-  if (N1 > 8192) return fail(JW_ERR_UNSUPPORTED, "FFT length %ld > 2^26", N);
+  if (N2 > 8192 && (!B || N2 > (1L << 26)))
+    return fail(JW_ERR_UNSUPPORTED, "FFT length %ld: three passes need a second workspace", N);
   // lines of 8192 points (N = 2^25, 2^26) stage 128 KB of LDS: past the 64 KB default
   auto lds_ok = [](auto kern, long M) -> hipError_t {
     const size_t b = (size_t)M * sizeof(cplx);
@@ -497,6 +531,24 @@ int run_fft(long N, long items, In1 in1, Out1 out_single, Out2 out_final, cplx* 
                        dim3(256), (size_t)N1 * sizeof(cplx), s, in1, a_out, N, N2, log1, T);
   }
   JW_HIP_TRY(hipGetLastError());
+  if constexpr (NEST) {
+    if (N2 > 8192) {
+    Tables T2;
+    if (int st = tables(N2, &T2); st != JW_OK) return st;
+    const long chunk = std::max(1L, 65535 / N1);  // inner items (rows) on grid.y <= 65535
+    const long N1i = split_n1(N2);
+    for (long it0 = 0; it0 < items; it0 += chunk) {
+      const long nit = std::min(chunk, items - it0);
+      const NestIn nin{A + it0 * N, N, N1, N2, N2 / N1i};
+      const NestOut<Out2> nout{out_final, N1, N1i, it0};
+      if (int st = run_fft<S, NestIn, NestOut<Out2>, NestOut<Out2>, false>(
+              N2, nit * N1, nin, nout, nout, B, s, T2, a_nt, false);
+          st != JW_OK)
+        return st;
+    }
+    return JW_OK;
+    }
+  }
   if (N2 == 512) {
     hipLaunchKernelGGL((pass512<S, false, false, RowIn, Out2>),
                        dim3((unsigned)(N1 / kT), (unsigned)items), dim3(512), 0, s, a_in, out_final,
@@ -547,14 +599,6 @@ int run_fft512_pipelined(long N, long items, long gsize, MkIn mk_in, MkOut mk_ou
   return JW_OK;
 }
 
-// The four-step split used for length N: N1 = N (one pass) for N <= 4096, else
-// N1 = 2^ceil(log2 N / 2), N2 = N / N1 (run_fft with long_ok = false).
-inline long split_n1(long N) {
-  if (N <= 4096) return N;
-  int logN = 0;
-  while ((1L << logN) < N) ++logN;
-  return 1L << ((logN + 1) / 2);
-}
 // The split run_fft takes for an input functor of the given kind (run_fft_long).
 inline long split_n1(long N, bool strided) {
   if (long_split(N)) return strided ? 512 : N / 512;

@@ -120,9 +120,23 @@ def test_lengths_past_2_24(n):
         assert nw(got, ex) < TOL_EXACT
 
 
-def test_length_past_2_26_refused():
-    with pytest.raises(NotImplementedError, match="2\\^26"):
-        CWT(MorletWavelet(*MORLET6)).transformFFT(np.zeros((1 << 26) + 1), np.array([4.0]), 1.0)
+@pytest.mark.parametrize("n,scales", [((1 << 26) + 1, (2.0, 900.0)), ((1 << 27) + 3, (900.0,))])
+def test_lengths_past_2_26_three_passes(n, scales):
+    # nextPowerOfTwo(n) = 2^27, 2^28 (ContinuousWaveletTransform.java:188-189, MathUtils.java:46-49:
+    # no cap in the reference): 8192-point columns, then the 16384 / 32768-point rows as two-pass
+    # FFTs of their own (three passes through two workspaces), every scale two-pass.  Per scale
+    # against the numpy restatement (correctly rounded FFT), at the same bar as 2^25 / 2^26.
+    scales = np.array(scales)
+    x = orc.fill_uniform(n, 9)
+    got = CWT(MorletWavelet(*MORLET6), PaddingType.ZERO).transformFFT(x, scales, 1.0).getCoefficients()
+    ref = np_cwt_morlet(x, scales, 1.0, MORLET6)
+    for i in range(len(scales)):
+        assert nw(got[i], ref[i]) < TOL_EXACT, (i, nw(got[i], ref[i]))
+
+
+def test_length_past_2_28_refused():
+    with pytest.raises(NotImplementedError, match="2\\^28"):
+        CWT(MorletWavelet(*MORLET6)).transformFFT(np.zeros((1 << 28) + 1), np.array([4.0]), 1.0)
 
 
 def test_batch_and_device_tensors(device):
