@@ -907,6 +907,16 @@ static void interp_weights(long P, long N, std::vector<double>& wt) {
     }
 }
 
+// One interpolation launch of the coarse-grid path: `items` rows of U (from row 0), signals
+// from sg0, of one group of equal M.
+struct InterpJob {
+  const cplx* U;
+  long M, P, sg0, items;
+  const BandScale* gb;
+  int gn;
+  const double* gw;
+};
+
 // Which path each scale of a jw_cwt_fft call takes (band kernel, coarse grid, two-pass), with
 // the wavelet's spectrum parameters: the rule cwt_fft_device runs and jw_cwt_fft_paths reports.
 struct CwtSplit {
@@ -1102,19 +1112,37 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   cplx* U = nullptr;
   double* dwt = nullptr;
   double4* wroots = nullptr;
-  std::vector<long> gchunk(groups.size());
+  std::vector<long> gchunk(groups.size()), uoff(groups.size(), 0);
   std::vector<Tables> gT(groups.size());
+  // JW_CWT_SPLIT=1: the coarse band kernels of every group and signal run first, on the side
+  // stream beside the two-pass chain (they are latency-bound, the chain HBM-bound), into one U
+  // per group; the interpolations (HBM-bound) follow the chain on the caller's stream.
+  const char* gsp = knob("JW_CWT_SPLIT");
+  bool split = gsp && gsp[0] == '1' && !coarse.empty() && pairs > 0;
   for (size_t g = 0; g < groups.size(); ++g)
     if ((st = fft::tables(groups[g].M, &gT[g])) != JW_OK) return st;
   if (!coarse.empty()) {
     JW_HIP_TRY(mem.alloc(&dcoarse, coarse.size() * sizeof(BandScale)));
     JW_HIP_TRY(upload_async(dcoarse, coarse.data(), coarse.size() * sizeof(BandScale), s));
-    long ubytes = 0, rtot = 0;
+    long ubytes = 0, rtot = 0, utotal = 0;
+    for (size_t g = 0; g < groups.size(); ++g)
+      utotal += (long)batch * groups[g].n * groups[g].M * (long)sizeof(cplx);
+    if (split) {  // every group's whole U at once: within 16 GB and a quarter of free HBM
+      size_t fr = 0, tot = 0;
+      if (hipMemGetInfo(&fr, &tot) != hipSuccess || utotal > (16L << 30) || (size_t)utotal > fr / 4)
+        split = false;
+      (void)hipGetLastError();
+    }
     std::vector<double> hwt;
     for (size_t g = 0; g < groups.size(); ++g) {
       const long per_sig = (long)groups[g].n * groups[g].M * (long)sizeof(cplx);
-      gchunk[g] = std::max(1L, std::min<long>(batch, (128L << 20) / per_sig));
-      ubytes = std::max(ubytes, gchunk[g] * per_sig);
+      gchunk[g] = split ? batch : std::max(1L, std::min<long>(batch, (128L << 20) / per_sig));
+      if (split) {
+        uoff[g] = ubytes / (long)sizeof(cplx);
+        ubytes += batch * per_sig;
+      } else {
+        ubytes = std::max(ubytes, gchunk[g] * per_sig);
+      }
       rtot += groups[g].M / 512;
       std::vector<double> wt;
       interp_weights(N / groups[g].M, N, wt);
@@ -1153,7 +1181,7 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
   // env JW_CWT_OVERLAP (A/B runs): 0 = never, 1 = whenever there are pairs.
   hipStream_t bs = s;
   const char* gov = knob("JW_CWT_OVERLAP");
-  const bool overlap = gov ? gov[0] != '0' : nband > 0;
+  const bool overlap = (gov ? gov[0] != '0' : nband > 0) || split;
   if (st == JW_OK && (nband > 0 || !coarse.empty()) && pairs > 0) {
     if (overlap) {
       SideStream* side = nullptr;
@@ -1211,6 +1239,32 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     }
     JW_HIP_TRY(hipGetLastError());
   }
+  const bool nt = (ntm & 2) != 0;
+  // interpolation of `items` coarse rows of one group (U rows from 0, signals from sg0)
+  auto interp_launch = [&](const InterpJob& j, hipStream_t is) -> int {
+    auto one = [&](auto lp) -> int {
+      constexpr int LP = decltype(lp)::value;
+      constexpr long TC = interp_tc<LP>();
+      const long chunks = (n + TC - 1) / TC, iblocks = j.items * chunks;
+      if (iblocks > 0x7fffffffL) return fail(JW_ERR_UNSUPPORTED, "CWT coarse grid too large");
+      hipLaunchKernelGGL(cwt_interp<LP>, dim3((unsigned)iblocks), dim3(256), 0, is, j.U, j.M,
+                         j.gb, j.gn, j.gw, N, n, ns, j.sg0, out, nt, T, (int)chunks);
+      return JW_OK;
+    };
+    int r;
+    switch (j.P) {
+      case 2: r = one(std::integral_constant<int, 1>{}); break;
+      case 4: r = one(std::integral_constant<int, 2>{}); break;
+      case 8: r = one(std::integral_constant<int, 3>{}); break;
+      case 16: r = one(std::integral_constant<int, 4>{}); break;
+      case 32: r = one(std::integral_constant<int, 5>{}); break;
+      default: r = one(std::integral_constant<int, 6>{}); break;
+    }
+    if (r != JW_OK) return r;
+    JW_HIP_TRY(hipGetLastError());
+    return JW_OK;
+  };
+  std::vector<InterpJob> deferred;  // JW_CWT_SPLIT: launched after the two-pass chain
   // coarse-grid scales: per group of equal M, the band kernel on the M-point grid into U, then
   // the Kaiser-Bessel interpolation to the N-point coefficients, a few signals at a time so
   // that U stays ~128 MB
@@ -1219,7 +1273,6 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
     // (cwt_band512_par); env JW_CWT_PAR=0 (A/B runs): one row group per workgroup
     const char* gpr = knob("JW_CWT_PAR");
     const bool use_par = !(gpr && gpr[0] == '0');
-    const bool nt = (ntm & 2) != 0;
     long woff = 0, roff = 0;
     // JW_TEST_CWT_FAIL_GROUP=k (tests only): fail at coarse group k, after groups < k have
     // launched on the side stream -- the error path must still join them (JoinGuard)
@@ -1247,6 +1300,7 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
       const double* gw = dwt + woff;
       woff += P * kInterpStride;
       roff += N1c;
+      cplx* const Ug = U + uoff[g];
 
       for (long sg0 = 0; sg0 < batch; sg0 += gchunk[g]) {
         const long cs = std::min<long>(gchunk[g], batch - sg0);
@@ -1258,32 +1312,19 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
         if (par) {
           hipLaunchKernelGGL(cwt_band512_par<CoarseOut>, dim3((unsigned)blocks), dim3(512), 0, bs,
                              Xn + sg0 * N, psi, gb, G.n, wN1c, M, N1c, items,
-                             CoarseOut{(double*)U, M, N1c, 0}, TM, N);
+                             CoarseOut{(double*)Ug, M, N1c, 0}, TM, N);
         } else {
           hipLaunchKernelGGL((cwt_band512<true, true, 6, CoarseOut>), dim3((unsigned)blocks),
                              dim3(512), 0, bs, Xn + sg0 * N, psi, gb, G.n, wN1c, M, N1c, items,
-                             CoarseOut{(double*)U, M, N1c, 0}, TM, 1, N);
+                             CoarseOut{(double*)Ug, M, N1c, 0}, TM, 1, N);
         }
         JW_HIP_TRY(hipGetLastError());
-        auto interp = [&](auto lp) -> int {
-          constexpr int LP = decltype(lp)::value;
-          constexpr long TC = interp_tc<LP>();
-          const long chunks = (n + TC - 1) / TC, iblocks = items * chunks;
-          if (iblocks > 0x7fffffffL) return fail(JW_ERR_UNSUPPORTED, "CWT coarse grid too large");
-          hipLaunchKernelGGL(cwt_interp<LP>, dim3((unsigned)iblocks), dim3(256), 0, bs, U, M, gb,
-                             G.n, gw, N, n, ns, sg0, out, nt, T, (int)chunks);
-          return JW_OK;
-        };
-        switch (P) {
-          case 2: st = interp(std::integral_constant<int, 1>{}); break;
-          case 4: st = interp(std::integral_constant<int, 2>{}); break;
-          case 8: st = interp(std::integral_constant<int, 3>{}); break;
-          case 16: st = interp(std::integral_constant<int, 4>{}); break;
-          case 32: st = interp(std::integral_constant<int, 5>{}); break;
-          default: st = interp(std::integral_constant<int, 6>{}); break;
+        const InterpJob job{Ug, M, P, sg0, items, gb, G.n, gw};
+        if (split) {
+          deferred.push_back(job);
+        } else if ((st = interp_launch(job, bs)) != JW_OK) {
+          return st;
         }
-        if (st != JW_OK) return st;
-        JW_HIP_TRY(hipGetLastError());
       }
     }
   }
@@ -1324,6 +1365,15 @@ int cwt_fft_device(int wavelet, const double* params, const double* x, long n,
       case JW_CWT_DOG: st = go(std::integral_constant<int, JW_CWT_DOG>{}); break;
       default: st = go(std::integral_constant<int, JW_CWT_MEYER>{}); break;
     }
+  }
+  if (!deferred.empty() && st == JW_OK) {
+    // the coarse band kernels (side stream) are done before their rows are interpolated here
+    if (join.side) {
+      JW_HIP_TRY(hipEventRecord(join.side->join, join.side->s));
+      JW_HIP_TRY(hipStreamWaitEvent(s, join.side->join, 0));
+    }
+    for (const InterpJob& j : deferred)
+      if ((st = interp_launch(j, s)) != JW_OK) return st;
   }
   return st;
 }

@@ -413,3 +413,18 @@ def test_error_after_side_stream_launches_joins(knobs):
     import torch
     torch.cuda.synchronize()
     assert np.array_equal(t.transformFFT(x, scales, 1.0).getCoefficients(), before)
+
+
+def test_split_coarse_path_bit_identical(knobs):
+    # JW_CWT_SPLIT=1 (A/B setting): every coarse-grid band kernel first, on the side stream beside
+    # the two-pass chain, into one workspace per group; the interpolations after the chain.  Same
+    # kernels on the same inputs: the same bits as the default order.
+    import torch
+    n = 1 << 18
+    scales = CWT.generateLogScales(2.0, 1024.0, 20)
+    xs = np.stack([orc.fill_uniform(n, 80 + b) for b in range(3)])
+    t = CWT(MorletWavelet(*MORLET6))
+    base = t.transformFFTBatch(torch.from_numpy(xs).cuda(), scales, 1.0).cpu().numpy()
+    knobs.setenv("JW_CWT_SPLIT", "1")
+    got = t.transformFFTBatch(torch.from_numpy(xs).cuda(), scales, 1.0).cpu().numpy()
+    assert np.array_equal(got, base)
