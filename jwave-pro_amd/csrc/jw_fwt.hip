@@ -488,6 +488,9 @@ constexpr int kRowMaxM = 20;  // longer filters keep the runtime-level kernels (
 #endif
 // row reverse: levels 2 .. 128 on one wave with wave-level syncs (A/B builds: 0)
 constexpr bool kRevSmallWave = JW_REV_SMALL_WAVE;
+#ifndef JW_FWT_NOROT
+#define JW_FWT_NOROT 0  // timing-only A/B builds: STRICT wrapped pairs in the plain order
+#endif
 constexpr bool kRevPairs2 = JW_REV_PAIRS2;  // row kernels: two outputs per lane (A/B builds: 0)
 
 template <bool FMA, int M, int H>
@@ -716,7 +719,7 @@ __device__ __forceinline__ void row_rev_level(double* buf, double* xs, int tid, 
       const int u = tid + r * kNT2;
       if (half >= kNT2 || u < half) {
         if (r == 0 && tid < 64) {  // wave-uniform: the wave holding u < M/2 - 1 (<= 19)
-          if constexpr (FMA) {
+          if constexpr (FMA || JW_FWT_NOROT) {  // JW_FWT_NOROT: timing-only builds (wrong order)
             double a0 = 0., a1 = 0.;
 #pragma unroll
             for (int t = (M >> 1) - 1; t >= 0; --t) {

@@ -327,6 +327,10 @@ int forward_cols(const ModwtPlan& p, const bool* fft, const cplx* F, const cplx*
     // and ran the forward 44.0 -> 48.5 ms)
     st = with_big_lc(g.C, [&](auto LCc) -> int {
       constexpr int LC = decltype(LCc)::value;
+      if (LC == 1024 && FT && use_wcol())
+        return launch_wcol(kp2p_w<ZPair, FwdMidT, OutPair>, (g.R / wcol::T) * 2 * nb, s,
+                           ZPair{Z, N}, FwdMidT{spec_h(FT, N, j), spec_g(FT, N, j), g.rbits, g.C},
+                           OutPair{Zi, N, nb * N}, g.rbits, 2 * nb, twf.p2, twi.p1);
       if (FT)
         return launch_grid<LC>(kp2p<LC, 1, ZPair, FwdMidT, OutPair>, (g.R / Geo<LC>::T) * 2 * nb,
                                s, ZPair{Z, N},
@@ -392,6 +396,10 @@ int inverse_cols(const ModwtPlan& p, const bool* fft, const cplx* F, const cplx*
     if (st != JW_OK) break;
     st = with_big_lc(g.C, [&](auto LCc) -> int {
       constexpr int LC = decltype(LCc)::value;
+      if (LC == 1024 && FT && use_wcol())
+        return launch_wcol(kp2p_w<RowsC, AdjMidT, OutF>, (g.R / wcol::T) * 2 * nb, s,
+                           RowsC{Zs, N}, AdjMidT{spec_g(FT, N, j), spec_h(FT, N, j), nb, g.rbits, g.C},
+                           OutF{Zi, N, 0}, g.rbits, 2 * nb, twf.p2, twi.p1);
       if (FT)
         return launch_grid<LC>(kp2p<LC, 1, RowsC, AdjMidT, OutF>, (g.R / Geo<LC>::T) * 2 * nb, s,
                                RowsC{Zs, N},

@@ -522,6 +522,188 @@ __global__ __launch_bounds__(kNT) void kline_modwt(In in, Mid mid, Out out, long
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// kp2p for 1024-point columns, 128-byte pieces at two workgroups per CU (round 6, A/B setting
+// JW_AUTO_WCOL).  The default kp2p<1024> holds 4 columns per workgroup in LDS (64-byte pieces,
+// ~3.3 TB/s); 8 columns of complex doubles need 128 KB of LDS (one workgroup per CU, measured
+// slower).  Here each column is one wavefront holding its 1024 points in registers, 16 per lane,
+// and the LDS only carries the exchanges between register stage groups -- real parts first, then
+// imaginary parts, through one double per point: 8 columns in 66 KB.  The butterflies, twiddles
+// and their order are stage_math's, so the values are kp2p's bit for bit.
+// ---------------------------------------------------------------------------------------
+namespace wcol {
+constexpr int LC = 1024, LOG = 10, EPT = 16, T = 8;
+// LDS slot of a point: one pad slot per 8 points.  Every layout below is lane-dependent base +
+// compile-time offset under it (so the exchanges address with immediates, no address registers),
+// and its 16-lane groups of 8-byte accesses hit distinct bank pairs (the rev(h) write aside);
+// columns start 4 doubles apart modulo the banks (the staging writes of 8 columns).
+constexpr int CSD = LC + LC / 8 + 4;  // 1156 doubles per column
+constexpr size_t LDS_BYTES = (size_t)T * CSD * sizeof(double);  // 74 KB: two workgroups per CU
+
+__device__ __forceinline__ int slot(int pos) { return pos + (pos >> 3); }
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+// Register layouts of a column's points over its wave: register k of lane l holds position
+// pos(l, k); in LDS that point sits at slot(pos) = base(l) + off(k), written out per layout so
+// every exchange addresses with immediate offsets.
+//   L04: stage group (t0 = 0, G = 4): pos = 16 l + k
+//   L44: group (4, 4):                pos = (l & 15) + 256 (l >> 4) + 16 k
+//   L82: group (8, 2):                pos = l + 64 (k >> 2) + 256 (k & 3)
+//   LNat: natural order:               pos = l + 64 k
+//   LRev: bit-reversed natural order:  pos = rev10(l + 64 k) = 16 rev6(l) + rev4(k)
+struct L04 {
+  static __device__ __forceinline__ int base(int l) { return 18 * l; }
+  static constexpr int off(int k) { return k + (k >> 3); }
+};
+struct L44 {
+  static __device__ __forceinline__ int base(int l) {
+    return (l & 15) + ((l & 15) >> 3) + 288 * (l >> 4);
+  }
+  static constexpr int off(int k) { return 18 * k; }
+};
+struct L82 {
+  static __device__ __forceinline__ int base(int l) { return l + (l >> 3); }
+  static constexpr int off(int k) { return 72 * (k >> 2) + 288 * (k & 3); }
+};
+struct LNat {
+  static __device__ __forceinline__ int base(int l) { return l + (l >> 3); }
+  static constexpr int off(int k) { return 72 * k; }
+};
+struct LRev {
+  static __device__ __forceinline__ int base(int l) { return 18 * brev(l, 6); }
+  static constexpr int rev4(int k) { return ((k & 1) << 3) | ((k & 2) << 1) | ((k & 4) >> 1) | ((k & 8) >> 3); }
+  static constexpr int off(int k) { return rev4(k) + (rev4(k) >> 3); }
+};
+// the stages t0 .. t0+G-1 on registers in layout (t0, G): stage_math with EPT = 16
+template <int G>
+__device__ __forceinline__ void stages(cplx (&v)[EPT], int lane, int t0, const cplx* __restrict__ tw) {
+  constexpr int E = 1 << G, NSET = EPT / E;
+  const int lowmask = (1 << t0) - 1;
+  int base[NSET];
+#pragma unroll
+  for (int i = 0; i < NSET; ++i) base[i] = set_base(lane + 64 * i, t0, G);
+#pragma unroll
+  for (int u = 0; u < G; ++u) {
+#pragma unroll
+    for (int i = 0; i < NSET; ++i) {
+      const int low = base[i] & lowmask;
+#pragma unroll
+      for (int r = 0; r < (1 << u); ++r) {
+        const cplx w = tw[(1 << (t0 + u)) + low + (r << t0)];
+#pragma unroll
+        for (int q = 0; q < (E >> (u + 1)); ++q) {
+          const int m = r + (q << (u + 1));
+          bfly(v[i * E + m], v[i * E + m + (1 << u)], w);
+        }
+      }
+    }
+    // one stage's twiddles live at a time (hoisted, the radix-16 group's 15 spilled)
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+// v moves from layout F to layout To in the wave's column (re, then im)
+template <class F, class To>
+__device__ __forceinline__ void xchg(cplx (&v)[EPT], double* col, int lane) {
+  double t[EPT];
+  double* const pf = col + F::base(lane);
+  double* const pt = col + To::base(lane);
+  wsync();
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) pf[F::off(k)] = v[k].x;
+  wsync();
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) t[k] = pt[To::off(k)];
+  wsync();
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) pf[F::off(k)] = v[k].y;
+  wsync();
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) v[k] = make_double2(t[k], pt[To::off(k)]);
+}
+// all 10 stages (groups (0,4), (4,4), (8,2)); v enters in layout (0,4), leaves in (8,2)
+__device__ __forceinline__ void run10(cplx (&v)[EPT], double* col, int lane,
+                                      const cplx* __restrict__ tw) {
+  stages<4>(v, lane, 0, tw);
+  xchg<L04, L44>(v, col, lane);
+  stages<4>(v, lane, 4, tw);
+  xchg<L44, L82>(v, col, lane);
+  stages<2>(v, lane, 8, tw);
+}
+}  // namespace wcol
+
+// pass 2 of a 1024-point column, one product (Mid), pass 1 of the next transform, rows out --
+// kp2p<1024, 1, ...> with 8 columns per workgroup (see wcol above)
+template <class In, class Mid, class Out>
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void kp2p_w(
+    In in, Mid mid, Out out, int wbits, long nitems, const cplx* __restrict__ tw2,
+    const cplx* __restrict__ tw1) {
+  using namespace wcol;
+  extern __shared__ double ldsd[];
+  int tile;
+  long item;
+  tile_item((1 << wbits) / T, nitems, &tile, &item);
+  const int c0 = tile * T;
+  const int tid = threadIdx.x, lane = tid & 63, cc = tid >> 6;
+  double* col = ldsd + cc * CSD;
+  cplx v[EPT];
+  {
+    // rows r = f / 8 of the 8 columns (128 bytes each), f = tid + 512 k, to the column's wave in
+    // layout L04 (position r): slot(r) = (tid >> 3) + (tid >> 6) + 72 k in column tid & 7
+    cplx g[EPT];
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+      const int f = tid + kNT * k;
+      g[k] = in(item, ((long)(f >> 3) << wbits) + c0 + (f & 7));
+    }
+    double t[EPT];
+    double* const pw = ldsd + (tid & 7) * CSD + (tid >> 3) + (tid >> 6);
+    double* const pr = col + L04::base(lane);
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) pw[72 * k] = g[k].x;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) t[k] = pr[L04::off(k)];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) pw[72 * k] = g[k].y;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) v[k] = make_double2(t[k], pr[L04::off(k)]);
+  }
+  run10(v, col, lane, tw2 + (long)(c0 + cc) * LC);
+  // to the natural positions h = lane + 64 k, the product, back at rev(h) for the next pass 1
+  xchg<L82, LNat>(v, col, lane);
+  const long l = c0 + cc;
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) v[k] = mid(0, item, ((long)(lane + 64 * k) << wbits) + l, v[k]);
+  xchg<LRev, L04>(v, col, lane);
+  run10(v, col, lane, tw1);
+  // rows out: column k / 2, position tid + 512 (k & 1) (f = tid + 512 k): 4 KB row pieces
+  double t[EPT];
+  double* const pw = col + L82::base(lane);
+  const double* const pr = ldsd + tid + (tid >> 3);
+  wsync();
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) pw[L82::off(k)] = v[k].x;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) t[k] = pr[(k >> 1) * CSD + 576 * (k & 1)];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) pw[L82::off(k)] = v[k].y;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int c = k >> 1, pos = tid + 512 * (k & 1);
+    out(0, item, (long)brev(c0 + c, wbits) * LC + pos,
+        make_double2(t[k], pr[(k >> 1) * CSD + 576 * (k & 1)]));
+  }
+}
+
 }  // namespace jf
 }  // namespace jw
 

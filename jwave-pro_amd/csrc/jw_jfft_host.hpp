@@ -92,6 +92,25 @@ int launch_grid(K kern, long blocks, hipStream_t s, A... args) {
   return JW_OK;
 }
 
+// kp2p_w (1024-point columns, 8 per workgroup): its own LDS size
+template <class K, class... A>
+int launch_wcol(K kern, long blocks, hipStream_t s, A... args) {
+  const size_t lds = wcol::LDS_BYTES;
+  JW_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)lds));
+  if (blocks <= 0) return JW_OK;
+  if (blocks >= (1L << 24))
+    return fail(JW_ERR_UNSUPPORTED, "Java-order FFT: grid of %ld workgroups", blocks);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kNT), lds, s, args...);
+  JW_HIP_TRY(hipGetLastError());
+  return JW_OK;
+}
+// JW_AUTO_WCOL=1 (A/B setting): kp2p's 1024-point columns through kp2p_w
+inline bool use_wcol() {
+  const char* e = knob("JW_AUTO_WCOL");
+  return e && e[0] == '1';
+}
+
 // ---------------------------------------------------------------------------------------
 // Functors (natural indices; see jw_jfft.hpp)
 // ---------------------------------------------------------------------------------------
