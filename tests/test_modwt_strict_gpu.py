@@ -337,3 +337,20 @@ def test_bluestein_three_pass_bit_exact(n, knobs):
         ref = orc.modwt_forward(xs[b], 3, g, h, "auto")
         assert bits_equal(c[b], ref), b
         assert bits_equal(xr[b], orc.modwt_inverse(ref, g, h, "auto")), b
+
+
+@pytest.mark.parametrize("n,J", [(1 << 20, 2), (1 << 19, 3)])
+def test_wave_column_kp2p_bit_exact(n, J, knobs):
+    # JW_AUTO_WCOL=1 (A/B setting, measured slower, profiles/r06/ab/auto_wcol): the 1024-point
+    # kp2p columns through kp2p_w (8 columns per workgroup, points in registers, re/im LDS
+    # exchanges) -- the same butterflies and twiddles, so the same bits as the reference path
+    knobs.setenv("JW_AUTO_WCOL", "1")
+    wv = W.Daubechies4()
+    g, h = ofilters(wv)
+    xs = np.stack([orc.fill_uniform(n, 5 + b) for b in range(2)])
+    m = MODWTTransform(wv)
+    c = m.forwardMODWT(xs, J)
+    xr = m.inverseMODWT(c)
+    for b in range(2):
+        assert bits_equal(c[b], orc.modwt_forward(xs[b], J, g, h, "auto")), b
+        assert bits_equal(xr[b], orc.modwt_inverse(c[b], g, h, "auto")), b
