@@ -96,3 +96,87 @@ def test_zero_skipping_variant_differs_on_nonfinite():
     x = orc.fill_uniform(32, 5)
     x[10] = math.inf
     assert not same(orc.modwt_forward(x, 4, g, h, "direct_nz"), orc.modwt_forward(x, 4, g, h, "direct"))
+
+
+# ---- FWT / WPT: Wavelet.forward / reverse (Wavelet.java:236-303) multiply every tap too ----
+def w_forward(a, h2, sD, wD):  # Wavelet.forward(arrTime, arrTimeLength) :236-262
+    out = [0.0] * h2
+    h = h2 >> 1
+    for i in range(h):
+        out[i] = out[i + h] = 0.0
+        for j in range(len(sD)):
+            k = (i << 1) + j
+            while k >= h2:
+                k -= h2
+            out[i] += a[k] * sD[j]
+            out[i + h] += a[k] * wD[j]
+    return out
+
+
+def w_reverse(a, h2, sR, wR):  # Wavelet.reverse(arrHilb, arrHilbLength) :277-303
+    out = [0.0] * h2
+    h = h2 >> 1
+    for i in range(h):
+        for j in range(len(sR)):
+            k = (i << 1) + j
+            while k >= h2:
+                k -= h2
+            out[k] += (a[i] * sR[j]) + (a[i + h] * wR[j])
+    return out
+
+
+def java_fwt(x, level, wv, rev):  # FastWaveletTransform.forward / reverse :71-153
+    arr, n, tw = list(x), len(x), wv.getTransformWavelength()
+    if not rev:
+        f = (wv.getScalingDeComposition(), wv.getWaveletDeComposition())
+        h, l = n, 0
+        while h >= tw and l < level:
+            arr[:h] = w_forward(arr, h, *f)
+            h, l = h >> 1, l + 1
+        return np.array(arr)
+    f = (wv.getScalingReConstruction(), wv.getWaveletReConstruction())
+    h = tw
+    for _ in range(level, n.bit_length() - 1):
+        h <<= 1
+    while tw <= h <= n:
+        arr[:h] = w_reverse(arr, h, *f)
+        h <<= 1
+    return np.array(arr)
+
+
+def java_wpt(x, level, wv, rev):  # WaveletPacketTransform.forward / reverse :60-191
+    arr, n, tw = list(x), len(x), wv.getTransformWavelength()
+    if not rev:
+        f = (wv.getScalingDeComposition(), wv.getWaveletDeComposition())
+        h, l = n, 0
+        while h >= tw and l < level:
+            for p in range(n // h):
+                arr[p * h:(p + 1) * h] = w_forward(arr[p * h:(p + 1) * h], h, *f)
+            h, l = h >> 1, l + 1
+        return np.array(arr)
+    f = (wv.getScalingReConstruction(), wv.getWaveletReConstruction())
+    h = tw
+    for _ in range(level, n.bit_length() - 1):
+        h <<= 1
+    while tw <= h <= n:
+        for p in range(n // h):
+            arr[p * h:(p + 1) * h] = w_reverse(arr[p * h:(p + 1) * h], h, *f)
+        h <<= 1
+    return np.array(arr)
+
+
+@pytest.mark.parametrize("wname,n", [("Haar1", 16), ("Daubechies4", 32), ("Symlet8", 16),
+                                     ("Daubechies8", 64)])
+def test_fwt_wpt_match_java_loops_nonfinite(wname, n):
+    rng = np.random.default_rng(n)
+    wv = W.by_name(wname)
+    lvl = n.bit_length() - 1
+    x = orc.fill_uniform(n, 4)
+    for p in rng.integers(0, n, 2):
+        x[p] = rng.choice([math.inf, -math.inf, math.nan])
+    with np.errstate(invalid="ignore", over="ignore"):
+        for level in (1, lvl):
+            assert same(orc.fwt_forward(x, level, wv), java_fwt(x, level, wv, False))
+            assert same(orc.fwt_reverse(x, level, wv), java_fwt(x, level, wv, True))
+            assert same(orc.wpt_forward(x, level, wv), java_wpt(x, level, wv, False))
+            assert same(orc.wpt_reverse(x, level, wv), java_wpt(x, level, wv, True))
