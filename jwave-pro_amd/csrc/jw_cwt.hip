@@ -541,6 +541,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #ifndef JW_CWT_PAR_PF
 #define JW_CWT_PAR_PF 1
 #endif
+// The lane's twiddles by recurrence (one complex product per block group, VALU that is ~7 % busy
+// here) instead of a dependent table gather: cfg3 2,374 -> 2,395 Msamples/s same box, accuracy
+// unchanged at the tests' bars (profiles/r06/ab/cwt_par_rec/); 0 = the table (A/B builds).
+#ifndef JW_CWT_PAR_REC
+#define JW_CWT_PAR_REC 1
+#endif
 template <class Out>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void cwt_band512_par(
     const cplx* __restrict__ Xn, const double* __restrict__ psi,
@@ -562,12 +568,29 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
   const double* xs = (const double*)(Xn + (long)sig * Nx + 64 * c + tr) + zc;
   const double* ps = psi + b.psi_off + 64 * c + tr;
   // blocks j0 + 2 jo (jo = 0, 1: two blocks of one parity per MFMA)
+#if JW_CWT_PAR_REC
+  // the lane's twiddle W_N1^(k1 (r0 + t)) by recurrence over its blocks (k1 steps by 4 per
+  // call of load; at most nb / 4 <= 31 products: ~1e-14 relative)
+  cplx wr = make_double2(0.0, 0.0), ws = make_double2(0.0, 0.0);
+  auto rec_init = [&](int par) {
+    const unsigned e = (((unsigned)b.b0 + par + 2 * jo) * ((unsigned)r0 + t)) & m1;
+    const double4 w0 = wN1[e], s4 = wN1[(4u * ((unsigned)r0 + t)) & m1];
+    wr = make_double2(w0.x, w0.y);
+    ws = make_double2(s4.x, s4.y);
+  };
+#endif
   auto load = [&](int j0, double (&xv)[4], double (&pv)[4], double& av) {
     const int j = j0 + 2 * jo;
     const bool in = j < b.nb;
     const int jj = in ? j : b.nb - 1;
-    const unsigned k1 = ((unsigned)b.b0 + jj) & m1, kx = ((unsigned)b.fb0 + jj) & mx;
+    const unsigned kx = ((unsigned)b.fb0 + jj) & mx;
+#if JW_CWT_PAR_REC
+    const cplx w = wr;
+    wr = fft::cmul(wr, ws);
+#else
+    const unsigned k1 = ((unsigned)b.b0 + jj) & m1;
     const double4 w = wN1[(k1 * ((unsigned)r0 + t)) & m1];
+#endif
     av = im_row ? (zc ? w.x : w.y) : (zc ? -w.y : w.x);
     av = in ? av : 0.0;
 #pragma unroll
@@ -580,6 +603,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = d4v{0.0, 0.0, 0.0, 0.0};
     double xv[4], pv[4], av;
+#if JW_CWT_PAR_REC
+    rec_init(par);
+#endif
     load(par, xv, pv, av);
     for (int j0 = par; j0 < b.nb; j0 += 4) {
 #if JW_CWT_PAR_PF  // the next pair's loads before this pair's MFMAs (16 more VGPRs)
