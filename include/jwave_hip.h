@@ -125,8 +125,9 @@ int jw_modwt_plan_filters(const jw_modwt_plan* plan, double* g, double* h);
  * pattern).  FFT levels run the
  * reference's circularConvolveFFT (:752-786) with its own FFT: radix 2 with recurrence
  * twiddles for powers of two (FastFourierTransform.java:172-212) and its Bluestein transform for
- * other lengths (:259-324), both bit-identical to the JVM for power-of-two n <= 2^28 and other
- * n <= 2^27 (transforms longer than 2^24 points run in three column passes) -- given that the
+ * other lengths (:259-324), both bit-identical to the JVM over the reference's own domain:
+ * power-of-two n <= 2^30 and other n <= 2^29 (Bluestein's m <= 2^30; past that the reference's
+ * int arithmetic overflows), transforms longer than 2^24 points in three column passes -- given that the
  * JVM's Math.sin/Math.cos are correctly rounded at the twiddle and chirp angles (Java specifies
  * them to 1 ulp; the engine and the oracle both take the correctly rounded value).
  * With a JW_ARITH_FMA plan (the fast contract) FFT runs the exact-twiddle frequency-domain
@@ -160,9 +161,11 @@ int jw_fft_reverse(const double* in_reim, double* out_reim, long n, int batch, i
  * algorithm operation for operation -- bit reversal, radix-2 decimation in time with the
  * recurrence twiddles wn = wn.mul(w) of every stage (:172-212), Complex.mul's (ac - bd, ad + bc),
  * Bluestein for other n (:259-324) -- so results are the JVM's bit for bit for power-of-two
- * n <= 2^28 and other n <= 2^27 (correctly rounded Math.sin/cos assumed, as above); longer
- * STRICT lines return JW_ERR_UNSUPPORTED.  JW_ARITH_FMA is jw_fft_forward / jw_fft_reverse
- * (correctly rounded twiddle tables). */
+ * n <= 2^30 and other n <= 2^29, the reference's own domain (a Java array holds at most 2^30 as a
+ * power of two; its Bluestein `int m` doubling overflows past n = 2^29, :261-265), correctly
+ * rounded Math.sin/cos assumed, as above; longer STRICT lines return JW_ERR_UNSUPPORTED.  Host
+ * tables past 2^26 take seconds to build (cached while they fit, jw_release_caches drops them).
+ * JW_ARITH_FMA is jw_fft_forward / jw_fft_reverse (correctly rounded twiddle tables). */
 int jw_fft_forward_ex(const double* in_reim, double* out_reim, long n, int batch, int arith,
                       int where, void* stream);
 int jw_fft_reverse_ex(const double* in_reim, double* out_reim, long n, int batch, int arith,

@@ -459,6 +459,23 @@ hipError_t upload_async(void* dst, const void* src, size_t bytes, hipStream_t s)
   }
   return e;
 }
+
+hipError_t upload_owned(void* dst, void* src, size_t bytes, hipStream_t s) {
+  hipError_t e = bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
+  if (e == hipSuccess) e = hipLaunchHostFunc(s, [](void* p) { std::free(p); }, src);
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(s);
+    std::free(src);
+  }
+  return e;
+}
+
+int host_threads() {
+  int t = 0;
+  if (const char* o = std::getenv("OMP_NUM_THREADS")) t = std::atoi(o);
+  if (t <= 0) t = (int)std::thread::hardware_concurrency();
+  return std::min(16, std::max(1, t));
+}
 }  // namespace jw
 
 using namespace jw;
@@ -646,15 +663,19 @@ static ModwtPath modwt_path(const ModwtPlan& p, int method, long n, int levels, 
 static int modwt_unsupported(int arith, int method, long n, const bool* fft, int levels) {
   int j = 1;
   while (j < levels && !fft[j]) ++j;
+  char lim[128];
+  if (arith == JW_ARITH_STRICT)
+    std::snprintf(lim, sizeof lim, "powers of two up to 2^%d (%ld) and other lengths up to 2^%d (%ld)",
+                  floor_log2(kStrictFftPow2Max), kStrictFftPow2Max, floor_log2(kStrictFftOtherMax),
+                  kStrictFftOtherMax);
+  else
+    std::snprintf(lim, sizeof lim, "2 <= N <= 2^%d (%ld)", floor_log2(kPyramidFftMax), kPyramidFftMax);
   return fail(JW_ERR_UNSUPPORTED,
               "MODWT FFT convolution (%s) at signal length %ld: level %d takes the FFT path "
               "(MODWTTransform.java:640-664) and this engine's %s FFT convolution supports %s; "
               "use ConvolutionMethod.DIRECT%s",
               method == JW_CONV_FFT ? "ConvolutionMethod.FFT" : "AUTO", n, j,
-              arith == JW_ARITH_STRICT ? "STRICT" : "FMA",
-              arith == JW_ARITH_STRICT
-                  ? "powers of two up to 2^28 (268435456) and other lengths up to 2^27 (134217728)"
-                  : "2 <= N <= 2^23 (8388608)",
+              arith == JW_ARITH_STRICT ? "STRICT" : "FMA", lim,
               method == JW_CONV_AUTO ? " or a larger fftConvolutionThreshold" : "");
 }
 
@@ -748,16 +769,17 @@ static int fft_call(int S, int arith, const double* in, double* out, long n, int
   if (st != JW_OK) return st;
   if (n == 0 || batch == 0) return JW_OK;
   if (!in || !out) return fail(JW_ERR_ILLEGAL_ARGUMENT, "data pointer is null");
-  // STRICT: the reference's own FFT (jw_jfft.hip): radix 2 for powers of two <= 2^24,
-  // Bluestein for other n <= 2^23
+  // STRICT: the reference's own FFT (jw_jfft.hip): radix 2 for powers of two, Bluestein for
+  // other n, over the reference's own domain (jw_internal.hpp kStrictFft*)
   const bool pow2 = (n & (n - 1)) == 0;
   const bool strict = arith == JW_ARITH_STRICT;
-  if (strict && n > (pow2 ? (1L << 28) : (1L << 27)))
+  if (strict && n > (pow2 ? kStrictFftPow2Max : kStrictFftOtherMax))
     return fail(JW_ERR_UNSUPPORTED,
                 "JW_ARITH_STRICT FFT (FastFourierTransform.java:112-324 operation for operation) "
-                "at length %ld: supported up to 2^28 (268435456) for powers of two and 2^27 "
-                "(134217728) otherwise (Bluestein's m <= 2^28); JW_ARITH_FMA runs any length",
-                n);
+                "at length %ld: supported up to 2^%d (%ld) for powers of two and 2^%d (%ld) "
+                "otherwise (Bluestein's m <= 2^%d), the reference's own int limits",
+                n, floor_log2(kStrictFftPow2Max), kStrictFftPow2Max, floor_log2(kStrictFftOtherMax),
+                kStrictFftOtherMax, floor_log2(kStrictFftPow2Max));
   return run_items(where, stream, in, (size_t)2 * n, out, (size_t)2 * n, batch,
                    [&](const double* di, double* dout, long nb, hipStream_t s) {
                      return strict ? fft_strict_device(S, di, dout, n, nb, s)

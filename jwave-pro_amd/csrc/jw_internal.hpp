@@ -173,6 +173,12 @@ int cached_table(DevCache<Key>& cache, const Key& key, size_t bytes, StreamAlloc
 // a host callback on the stream frees once the transfer has been reached (the caller's
 // buffer may go away as soon as this returns).
 hipError_t upload_async(void* dst, const void* src, size_t bytes, hipStream_t s);
+// The same without the staging copy, for multi-GB tables: src comes from std::malloc and is
+// owned by the stream from here on (freed by a host callback once the transfer is reached; on
+// an error, after a stream synchronize).
+hipError_t upload_owned(void* dst, void* src, size_t bytes, hipStream_t s);
+// Host threads for table builds: OMP_NUM_THREADS when set, else the machine's, at most 16.
+int host_threads();
 
 // Correctly rounded sin and cos of x (jw_crmath.cc): the values of Math.sin / Math.cos the
 // STRICT FFT tables use.
@@ -208,11 +214,14 @@ int modwt_inverse_device(const ModwtPlan& p, const double* coeffs, double* x, lo
                          int batch, hipStream_t s);
 // FFT-path length ranges (inclusive, n >= 2).  The FMA pyramid (jw_modwt_fft.hip) takes
 // n <= kPyramidFftMax; STRICT (JWave's own FFT, jw_jfft.hip) takes powers of two up to
-// kStrictFftPow2Max and other n up to kStrictFftOtherMax (Bluestein, m <= 2^28).  A STRICT level
-// outside its range is JW_ERR_UNSUPPORTED, never the pyramid (not JWave's arithmetic): that is
-// only sound while the STRICT range covers the pyramid's, which the assertion pins.
+// kStrictFftPow2Max and other n up to kStrictFftOtherMax (Bluestein, m <= 2^30).  Those are the
+// reference's own limits: a Java int array length caps the powers of two at 2^30, and past
+// n = 2^29 Bluestein's `int m` doubling loop (FastFourierTransform.java:261-265) overflows.  A
+// STRICT level outside its range is JW_ERR_UNSUPPORTED, never the pyramid (not JWave's
+// arithmetic): that is only sound while the STRICT range covers the pyramid's, which the
+// assertion pins.
 constexpr long kPyramidFftMax = 1L << 23;
-constexpr long kStrictFftPow2Max = 1L << 28;
+constexpr long kStrictFftPow2Max = 1L << 30;
 constexpr long kStrictFftOtherMax = kStrictFftPow2Max / 2;
 static_assert(kPyramidFftMax <= kStrictFftOtherMax && kStrictFftOtherMax <= kStrictFftPow2Max,
               "the STRICT FFT range must contain the FMA pyramid's");

@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <tuple>
 #include <type_traits>
 #include <vector>
@@ -30,21 +31,44 @@ DevCache<TwKey> g_tw(kCacheBytes);
 
 constexpr double kJavaPi = 3.141592653589793;  // Math.PI
 
-void java_twiddles(long n, bool inverse, std::vector<cplx>& tw) {
-  tw.assign(n, make_double2(0.0, 0.0));
-  for (long half = 1; half < n; half <<= 1) {
-    const long size = 2 * half;
+// The reference's twiddles of the stages half = 2^t, t in [t0, t1) (:188-201): put(idx, wn_k) for
+// idx = half + k, k < half, in recurrence order.
+template <class Put>
+void java_stages(int t0, int t1, bool inverse, const Put& put) {
+  for (int t = t0; t < t1; ++t) {
+    const long half = 1L << t, size = 2 * half;
     const double angle = 2 * kJavaPi / (double)size * (double)(inverse ? 1 : -1);
     double wr, wi;  // Math.cos(angle), Math.sin(angle), correctly rounded (jw_crmath.cc)
     cr_sincos(angle, &wi, &wr);
     double nr = 1.0, ni = 0.0;  // wn = new Complex(1, 0)
     for (long k = 0; k < half; ++k) {
-      tw[half + k] = make_double2(nr, ni);
+      put(half + k, make_double2(nr, ni));
       const double tr = nr * wr - ni * wi, ti = nr * wi + ni * wr;  // wn = wn.mul(w)
       nr = tr;
       ni = ti;
     }
   }
+}
+
+// Tw[idx] (idx = 1 .. n - 1) of an n-point transform, scattered by put straight into a device
+// layout (no n-entry staging table: 16 GB at 2^30).  Each stage is one sequential recurrence and
+// the longest two are half and a quarter of the work, so they run on threads of their own.
+template <class Put>
+void java_twiddles(long n, bool inverse, const Put& put) {
+  const int lg = ilog2(n);
+  if (n < (1L << 22) || host_threads() < 3) {
+    java_stages(0, lg, inverse, put);
+    return;
+  }
+  std::thread top([&] { java_stages(lg - 1, lg, inverse, put); });
+  std::thread next([&] { java_stages(lg - 2, lg - 1, inverse, put); });
+  java_stages(0, lg - 2, inverse, put);
+  top.join();
+  next.join();
+}
+
+cplx* host_table(size_t entries) {
+  return static_cast<cplx*>(std::malloc(entries * sizeof(cplx)));
 }
 
 }  // namespace
@@ -57,17 +81,19 @@ int twiddles(long n, bool inverse, int lc1, Tw* out, StreamAllocs& mem, hipStrea
   const void* p = nullptr;
   int st = cached_table(g_tw, TwKey(dev, n, inverse ? 1 : 0, lc1), entries * sizeof(cplx), mem,
                         s, &p, [&](void* d) -> int {
-                          std::vector<cplx> tw;
-                          java_twiddles(n, inverse, tw);
-                          std::vector<cplx> h(entries);
-                          std::copy(tw.begin(), tw.begin() + (one ? n : lc1), h.begin());
-                          if (!one) {
-                            const long lc2 = n / lc1;
-                            for (long l = 0; l < lc1; ++l)
-                              for (long m = 0; m < lc2; ++m)
-                                h[lc1 + l * lc2 + m] = tw[m * lc1 + l];
-                          }
-                          JW_HIP_TRY(upload_async(d, h.data(), entries * sizeof(cplx), s));
+                          cplx* h = host_table(entries);
+                          if (!h) return fail(JW_ERR_NO_MEMORY, "twiddle table: %zu entries", entries);
+                          const cplx zero = make_double2(0.0, 0.0);
+                          h[0] = zero;  // Tw[0] is never read
+                          const long lc2 = one ? 1 : n / lc1;
+                          const int lb = ilog2(one ? n : lc1);
+                          cplx* h2 = h + lc1;  // h2[l lc2 + m] = Tw[m lc1 + l]
+                          if (!one) h2[0] = zero;
+                          java_twiddles(n, inverse, [&](long idx, cplx w) {
+                            if (idx < lc1 || one) h[idx] = w;
+                            if (!one) h2[(idx & (lc1 - 1)) * lc2 + (idx >> lb)] = w;
+                          });
+                          JW_HIP_TRY(upload_owned(d, h, entries * sizeof(cplx), s));
                           return JW_OK;
                         });
   if (st != JW_OK) return st;
@@ -86,10 +112,12 @@ long three_pass_min() {
 }
 
 using Tw3Key = std::tuple<int, long, int>;  // device, n, inverse (the split is a function of n)
-// The three-pass tables are (A + AB + n) x 16 bytes: 1.08 GB at 2^26, 4.3 GB at 2^28 per
-// direction.  Their own budget holds both directions at 2^28, so the longest transforms keep
-// their tables instead of rebuilding multi-GB host tables on every call.
-DevCache<Tw3Key> g_tw3(10UL << 30);
+// The three-pass tables are (A + AB + n) x 16 bytes: 1.08 GB at 2^26, 4.3 GB at 2^28, 17.2 GB at
+// 2^30 per direction.  Their own budget holds both directions at 2^30, so the longest transforms
+// keep their tables instead of rebuilding multi-GB host tables on every call; a table
+// is kept only while it also fits a quarter of the free device memory (cached_table), and
+// jw_release_caches drops them.
+DevCache<Tw3Key> g_tw3(36UL << 30);
 
 int twiddles3(long n, bool inverse, Tw3* out, StreamAllocs& mem, hipStream_t s) {
   int dev = 0;
@@ -101,17 +129,17 @@ int twiddles3(long n, bool inverse, Tw3* out, StreamAllocs& mem, hipStream_t s) 
   const void* p = nullptr;
   int st = cached_table(g_tw3, Tw3Key(dev, n, inverse ? 1 : 0), entries * sizeof(cplx), mem, s, &p,
                         [&](void* d) -> int {
-                          std::vector<cplx> tw;
-                          java_twiddles(n, inverse, tw);
-                          std::vector<cplx> h(entries);
-                          std::copy(tw.begin(), tw.begin() + A, h.begin());
-                          cplx* pm = h.data() + A;
-                          for (long l = 0; l < A; ++l)
-                            for (long m = 0; m < B; ++m) pm[l * B + m] = tw[m * A + l];
-                          cplx* p3 = pm + AB;
-                          for (long l = 0; l < AB; ++l)
-                            for (long m = 0; m < C; ++m) p3[l * C + m] = tw[m * AB + l];
-                          JW_HIP_TRY(upload_async(d, h.data(), entries * sizeof(cplx), s));
+                          cplx* h = host_table(entries);
+                          if (!h) return fail(JW_ERR_NO_MEMORY, "twiddle table: %zu entries", entries);
+                          cplx* pm = h + A;   // pm[l B + m] = Tw[m A + l]
+                          cplx* p3 = pm + AB; // p3[l C + m] = Tw[m A B + l]
+                          h[0] = pm[0] = p3[0] = make_double2(0.0, 0.0);  // Tw[0]: never read
+                          java_twiddles(n, inverse, [&](long idx, cplx w) {
+                            if (idx < A) h[idx] = w;
+                            if (idx < AB) pm[(idx & (A - 1)) * B + (idx >> a)] = w;
+                            p3[(idx & (AB - 1)) * C + (idx >> (a + b))] = w;
+                          });
+                          JW_HIP_TRY(upload_owned(d, h, entries * sizeof(cplx), s));
                           return JW_OK;
                         });
   if (st != JW_OK) return st;
@@ -589,8 +617,8 @@ int modwt_strict(bool inverse, const ModwtPlan& p, const double* in, double* out
 // ---------------------------------------------------------------------------------------
 // entry points (jw_internal.hpp)
 // ---------------------------------------------------------------------------------------
-// every length the reference's FFT path takes here: powers of two (radix 2) up to 2^28 and,
-// through Bluestein with m <= 2^28, any other n <= 2^27
+// every length the reference's FFT path takes: powers of two (radix 2) up to 2^30 and, through
+// Bluestein with m <= 2^30, any other n <= 2^29 (jw_internal.hpp kStrictFft*)
 bool modwt_strict_fft_supported(long n) {
   return n >= 2 && n <= ((n & (n - 1)) == 0 ? kStrictFftPow2Max : kStrictFftOtherMax);
 }
@@ -615,11 +643,11 @@ int fft_strict_device(int S, const double* in, double* out, long n, long batch, 
   }
   if ((n & (n - 1)) != 0) {
     if (n > kStrictFftOtherMax)
-      return fail(JW_ERR_UNSUPPORTED, "Java-order FFT: length %ld > 2^27", n);
+      return fail(JW_ERR_UNSUPPORTED, "Java-order FFT: length %ld > %ld", n, kStrictFftOtherMax);
     return jf::bs_fft_strict(S > 0, (const jf::cplx*)in, (jf::cplx*)out, n, batch, s);
   }
   if (n > jf::kStrictPow2Max)
-    return fail(JW_ERR_UNSUPPORTED, "Java-order FFT: length %ld > 2^28", n);
+    return fail(JW_ERR_UNSUPPORTED, "Java-order FFT: length %ld > %ld", n, jf::kStrictPow2Max);
   // in == out is safe: a line is read whole before it is written, and the column path reads
   // the input in pass 1 and writes the output in pass 2 (from the workspace Z)
   StreamAllocs mem(s);

@@ -11,6 +11,8 @@
 // chirp and FFT_m(b) depend on (n, direction) only: built once (host cos / sin in the
 // reference's expression, the m-point transform on the device) and cached.
 #include <cmath>
+#include <cstdlib>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -46,24 +48,42 @@ int bs_tables(long n, bool inverse, BsTab* out, StreamAllocs& mem, hipStream_t s
   const int st = cached_table(
       g_bst, BsKey(dev, n, inverse ? 1 : 0), (size_t)(n + m) * sizeof(cplx), mem, s, &p,
       [&](void* d) -> int {
-        std::vector<cplx> h((size_t)(n + m), make_double2(0.0, 0.0));
-        cplx* chirp = h.data();
-        for (long i = 0; i < n; ++i) {  // :268-272
-          const double angle = kJavaPi * (double)i * (double)i / (double)n * (inverse ? 1 : -1);
-          double c, sn;  // Math.cos / Math.sin, correctly rounded (jw_crmath.cc)
-          cr_sincos(angle, &sn, &c);
-          chirp[i] = make_double2(c, sn);
+        cplx* chirp = static_cast<cplx*>(std::malloc((size_t)n * sizeof(cplx)));
+        cplx* b = static_cast<cplx*>(std::calloc((size_t)m, sizeof(cplx)));
+        if (!chirp || !b) {
+          std::free(chirp);
+          std::free(b);
+          return fail(JW_ERR_NO_MEMORY, "Bluestein tables: n = %ld, m = %ld", n, m);
         }
-        cplx* b = chirp + n;  // :285-290, conjugate() = (r, -j)
-        b[0] = make_double2(chirp[0].x, -chirp[0].y);
+        // :268-272, one angle per index: ~0.5 us each past 2^20 (the correctly rounded
+        // sin / cos of arguments up to pi n), so long chirps are split over host threads
+        auto fill = [&](long lo, long hi) {
+          for (long i = lo; i < hi; ++i) {
+            const double angle = kJavaPi * (double)i * (double)i / (double)n * (inverse ? 1 : -1);
+            double c, sn;  // Math.cos / Math.sin, correctly rounded (jw_crmath.cc)
+            cr_sincos(angle, &sn, &c);
+            chirp[i] = make_double2(c, sn);
+          }
+        };
+        const int nt = n >= (1L << 16) ? host_threads() : 1;
+        std::vector<std::thread> pool;
+        for (int t = 1; t < nt; ++t) pool.emplace_back(fill, n * t / nt, n * (t + 1) / nt);
+        fill(0, n / nt);
+        for (auto& th : pool) th.join();
+        b[0] = make_double2(chirp[0].x, -chirp[0].y);  // :285-290, conjugate() = (r, -j)
         for (long i = 1; i < n; ++i) {
           b[i] = make_double2(chirp[i].x, -chirp[i].y);
           b[m - i] = make_double2(chirp[i].x, -chirp[i].y);
         }
         cplx* dev_b = nullptr;
-        JW_HIP_TRY(mem.alloc(&dev_b, (size_t)m * sizeof(cplx)));
-        JW_HIP_TRY(upload_async(d, h.data(), (size_t)n * sizeof(cplx), s));
-        JW_HIP_TRY(upload_async(dev_b, b, (size_t)m * sizeof(cplx), s));
+        hipError_t e = mem.alloc(&dev_b, (size_t)m * sizeof(cplx));
+        if (e != hipSuccess) {
+          std::free(chirp);
+          std::free(b);
+          JW_HIP_TRY(e);
+        }
+        JW_HIP_TRY(upload_owned(d, chirp, (size_t)n * sizeof(cplx), s));
+        JW_HIP_TRY(upload_owned(dev_b, b, (size_t)m * sizeof(cplx), s));
         // fftCooleyTukeyInternal(b, false) (:294)
         return fft_rows(m, false, 1, RowsC{dev_b, m}, OutCS{(cplx*)d + n, m, 1.0, 0}, mem, s);
       });
@@ -157,7 +177,7 @@ struct OutMulB {
 };
 
 // The convolution of fftBluestein with three-pass m-point transforms (m >= three_pass_min(),
-// up to 2^28): FFT_m(a) = passes 1..3 (the last one multiplying by B), IFFT_m of the product =
+// up to 2^30): FFT_m(a) = passes 1..3 (the last one multiplying by B), IFFT_m of the product =
 // passes 1..3 into Post.  Same operations in the same order as the two-pass chain below.
 int bs_conv3(long m, long items, const Pre& pre, const Post& post, const cplx* B,
              StreamAllocs& mem, hipStream_t s) {

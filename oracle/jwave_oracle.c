@@ -313,6 +313,8 @@ static void fft_bluestein(double* x, long n, int inverse) {
   double* chirp = (double*)malloc(sizeof(double) * 2 * n);
   double* a = (double*)calloc(2 * m, sizeof(double));
   double* b = (double*)calloc(2 * m, sizeof(double));
+  /* one independent angle per index (:268-272); threads only share the work out */
+#pragma omp parallel for schedule(static) if (n >= (1L << 16))
   for (long i = 0; i < n; i++) {
     double angle = JAVA_PI * (double)i * (double)i / (double)n * (inverse ? 1 : -1);
     java_sincos(angle, &chirp[2 * i + 1], &chirp[2 * i]);
@@ -345,6 +347,23 @@ static void fft_bluestein(double* x, long n, int inverse) {
     x[2 * i] = rr; x[2 * i + 1] = ri;
   }
   free(chirp); free(a); free(b);
+}
+
+/* The twiddles one stage of fftCooleyTukey uses (:188-201): wn_k, k < size / 2, by the
+ * recurrence wn = wn.mul(w) from (1, 0) -- the same in every block of the stage, and the same
+ * whatever n (the angle is 2 pi / size).  Test helper: the last stage of an n-point transform
+ * combines the n/2-point transforms of the even and odd samples with these. */
+void jwo_fft_stage_twiddles(long size, int inverse, double* out) {
+  double angle = 2 * JAVA_PI / (double)size * (inverse ? 1 : -1);
+  double wr, wi;
+  java_sincos(angle, &wi, &wr);
+  double nr = 1, ni = 0;
+  for (long k = 0; k < size / 2; k++) {
+    out[2 * k] = nr;
+    out[2 * k + 1] = ni;
+    double nnr = nr * wr - ni * wi, nni = nr * wi + ni * wr;
+    nr = nnr; ni = nni;
+  }
 }
 
 void jwo_fft(double* reim, long n, int inverse) {

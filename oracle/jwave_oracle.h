@@ -71,6 +71,7 @@ int  jwo_modwt_auto_uses_fft(long N, long M, int threshold);
 /* In-place on interleaved (re,im) of length n.  Power of 2 -> Cooley-Tukey with
  * recurrence twiddles; otherwise Bluestein.  inverse scales by 1/n. */
 void jwo_fft(double* reim, long n, int inverse);
+void jwo_fft_stage_twiddles(long size, int inverse, double* out);
 void jwo_set_exact_twiddles(int on); /* test switch, see jwave_oracle.c */
 
 /* ---- FWT (transforms/wavelets/Wavelet.java:236-303, FastWaveletTransform.java:71-153) ---- */

@@ -111,6 +111,13 @@ def fft(x, inverse=False):
     return buf[0::2] + 1j * buf[1::2]
 
 
+def fft_stage_twiddles(size, inverse=False):
+    """wn_k (k < size / 2) of fftCooleyTukey's stage of this size (FastFourierTransform.java:188-201)."""
+    buf = np.empty(size)
+    lib().jwo_fft_stage_twiddles(ctypes.c_long(size), 1 if inverse else 0, _p(buf))
+    return buf.view(np.complex128)  # (re, im) pairs: the values as computed, no arithmetic
+
+
 def fwt_forward(x, level, wavelet):
     x = _f64(x)
     y = np.empty_like(x)

@@ -377,22 +377,26 @@ def test_fft_levels_past_2_23_are_unsupported_not_direct():
     # JWave runs these levels through its FFT convolution (MODWTTransform.java:640-664,
     # FastFourierTransform.java:112-164); the engine's FFT paths stop at 2^23, so the call must
     # fail with the limit named instead of returning DIRECT values (~1e-10 away).
-    # STRICT (JWave's FFT): powers of two to 2^28, Bluestein to 2^27; FMA's pyramid: 2^23
+    # STRICT (JWave's FFT): powers of two to 2^30, Bluestein to 2^29 (the reference's own int
+    # limits); FMA's pyramid: 2^23
     lib = _native.lib()
     J = 2
     vp = ctypes.c_void_p
-    for arith, method, n, lim in ((_native.JW_ARITH_STRICT, _native.JW_CONV_AUTO, (1 << 27) + 2, "2^27"),
-                                  (_native.JW_ARITH_STRICT, _native.JW_CONV_FFT, (1 << 27) + 2, "2^27"),
-                                  (_native.JW_ARITH_FMA, _native.JW_CONV_FFT, (1 << 23) + 2, "2^23")):
-        x = np.zeros(n)  # calloc / untouched pages: nothing is read before the check
-        c = np.zeros((J + 1) * n)
+    for arith, method, n, lim, where in (
+            # (2^29 + 1000) * 8 wraps to 8000 > 4096 in the int32 rule: level 1 is FFT
+            (_native.JW_ARITH_STRICT, _native.JW_CONV_AUTO, (1 << 29) + 1000, "2^29", _native.JW_DEVICE),
+            (_native.JW_ARITH_STRICT, _native.JW_CONV_FFT, (1 << 29) + 1000, "2^29", _native.JW_DEVICE),
+            (_native.JW_ARITH_FMA, _native.JW_CONV_FFT, (1 << 23) + 2, "2^23", _native.JW_HOST)):
+        # JW_HOST: calloc'd, untouched pages; JW_DEVICE: the range check precedes every access
+        x = np.zeros(n if where == _native.JW_HOST else 1)
+        c = np.zeros((J + 1) * n if where == _native.JW_HOST else 1)
         wv = W.Daubechies4()
         sd, wd = np.asarray(wv.getScalingDeComposition()), np.asarray(wv.getWaveletDeComposition())
         plan = vp()
         assert lib.jw_modwt_plan_create(ctypes.byref(plan), vp(sd.ctypes.data), vp(wd.ctypes.data),
                                         8, 4096, arith) == _native.JW_OK
         for fn, a, b in ((lib.jw_modwt_forward, x, c), (lib.jw_modwt_inverse, c, x)):
-            st = fn(plan, vp(a.ctypes.data), vp(b.ctypes.data), n, J, 1, method, _native.JW_HOST, None)
+            st = fn(plan, vp(a.ctypes.data), vp(b.ctypes.data), n, J, 1, method, where, None)
             assert st == _native.JW_ERR_UNSUPPORTED, (arith, method, st)
             msg = _native.last_error()
             assert lim in msg and str(n) in msg and "level 1" in msg, msg
@@ -406,16 +410,19 @@ def test_fft_levels_past_2_23_are_unsupported_not_direct():
 
 
 def test_strict_fft_past_its_range_is_unsupported():
-    # STRICT runs the reference's FFT for powers of two up to 2^28 (three column passes past
-    # 2^24) and Bluestein up to 2^27 (m <= 2^28); past those, an error naming the limits
+    # STRICT runs the reference's FFT for powers of two up to 2^30 (three column passes past
+    # 2^24) and Bluestein up to 2^29 (m <= 2^30) -- the reference's own domain: a Java array
+    # holds at most 2^30 as a power of two, and its Bluestein `int m` doubling overflows past
+    # n = 2^29 (FastFourierTransform.java:261-265); past those, an error naming the limits
     lib = _native.lib()
     vp = ctypes.c_void_p
-    for n in ((1 << 27) + 2, 1 << 29):
-        z = np.zeros(2 * n)  # calloc: pages untouched
+    z = np.zeros(2)  # JW_DEVICE: the range check precedes every access
+    for n in ((1 << 29) + 1, (1 << 30) - 1, 1 << 31):
         st = lib.jw_fft_forward_ex(vp(z.ctypes.data), vp(z.ctypes.data), n, 1,
-                                   _native.JW_ARITH_STRICT, _native.JW_HOST, None)
+                                   _native.JW_ARITH_STRICT, _native.JW_DEVICE, None)
         msg = _native.last_error()
-        assert st == _native.JW_ERR_UNSUPPORTED and "2^28" in msg and "2^27" in msg, msg
+        assert st == _native.JW_ERR_UNSUPPORTED and "2^30" in msg and "2^29" in msg, msg
+        assert "(1073741824)" in msg and "(536870912)" in msg, msg
 
 
 def test_strict_range_contains_the_pyramid_range():
@@ -426,7 +433,7 @@ def test_strict_range_contains_the_pyramid_range():
     vp = ctypes.c_void_p
     wv = W.Daubechies4()
     sd, wd = np.asarray(wv.getScalingDeComposition()), np.asarray(wv.getWaveletDeComposition())
-    n = 1 << 29
+    n = (1 << 30) + 2
     x = np.zeros(1)
     msgs = {}
     for arith in (_native.JW_ARITH_STRICT, _native.JW_ARITH_FMA):
@@ -442,7 +449,7 @@ def test_strict_range_contains_the_pyramid_range():
     lim = {a: [int(v) for v in re.findall(r"\((\d+)\)", m)] for a, m in msgs.items()}
     pow2_max, other_max = lim[_native.JW_ARITH_STRICT]
     (pyr_max,) = lim[_native.JW_ARITH_FMA]
-    assert (pow2_max, other_max, pyr_max) == (1 << 28, 1 << 27, 1 << 23)
+    assert (pow2_max, other_max, pyr_max) == (1 << 30, 1 << 29, 1 << 23)
     assert pyr_max <= other_max <= pow2_max
 
 
