@@ -77,6 +77,9 @@ def host_cpu():
     return threads, {"host_cpus": os.cpu_count(), "affinity_cpus": affinity, "cpu_model": model}
 
 
+REHEARSAL = {}  # JW_BENCH_SHARE_GPU=1: added to the JSON line (main)
+
+
 def spawn_ranks(n):
     """bench.py --gpus N without a launcher: start N rank processes of this script (one per
     GPU, RANK = LOCAL_RANK = r, rendezvous on 127.0.0.1) and return the worst exit code.  This
@@ -303,7 +306,7 @@ def main_cwt(args, dev, rank, world):
                                  f"and {n_band} through the one-pass band kernel (DESIGN.md 5.4; "
                                  "split from jw_cwt_fft_paths)",
                          "scale_split": {"two_pass": n_two, "band": n_band, "coarse_grid": n_coarse}},
-            "cpu_baseline": cpu}), flush=True)
+            "cpu_baseline": cpu, **REHEARSAL}), flush=True)
 
 
 def main_fwt2d(args, dev, rank, world):
@@ -408,7 +411,7 @@ def main_fwt2d(args, dev, rank, world):
                          "traffic": step_traffic("fwt2d", B == 64),
                          "algorithmic_bytes_per_step": per, "fwd_ms": round(fms, 3),
                          "rev_ms": round(rms_, 3)},
-            "cpu_baseline": cpu}), flush=True)
+            "cpu_baseline": cpu, **REHEARSAL}), flush=True)
 
 
 def launch_check(args, rank, local_rank, world):
@@ -435,11 +438,21 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.launch_check:
         return launch_check(args, rank, local_rank, world)
+    # JW_BENCH_SHARE_GPU=1 (rehearsal of the multi-rank path on a box with fewer GPUs than
+    # ranks; never set by the driver): rank r runs on GPU r mod count, over gloo (RCCL takes
+    # one rank per GPU), and the JSON line says so -- a check that the ranks shard, time and
+    # reduce correctly on hardware, not a scaling number
+    share = os.environ.get("JW_BENCH_SHARE_GPU") == "1"
+    if share:
+        local_rank %= torch.cuda.device_count()
+        REHEARSAL["shared_gpu_rehearsal"] = {
+            "ranks": world, "gpus": torch.cuda.device_count(), "backend": "gloo",
+            "note": "ranks share GPUs: checks sharding, timing and reductions, not scaling"}
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
         from jwave import distributed as jdist
-        jdist.init_from_env("nccl", device=dev)
+        jdist.init_from_env("gloo" if share else "nccl", device=None if share else dev)
         world = dist.get_world_size()  # the RCCL communicator's size (echoed as n_gpus)
     if args.workload == "cwt":
         return main_cwt(args, dev, rank, world)
@@ -787,6 +800,7 @@ def main():
             out["host_path"], out["auto_path"] = extra_paths()
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.wavelet, n, J)
+        out.update(REHEARSAL)
         print(json.dumps(out), flush=True)
 
     if world > 1:

@@ -30,27 +30,29 @@ def shard_range(n_items, rank, world):
     return start, base + (1 if rank < extra else 0)
 
 
-def _device():
+def _device(device=None):
+    """Where a collective's tensor lives: the rank's GPU under RCCL, host memory under gloo
+    (whatever device the caller names)."""
     if dist.get_backend() == "nccl":
-        return torch.device("cuda", torch.cuda.current_device())
+        return device or torch.device("cuda", torch.cuda.current_device())
     return torch.device("cpu")
 
 
 def max_over_ranks(value, device=None):
-    t = torch.tensor([float(value)], dtype=torch.float64, device=device or _device())
+    t = torch.tensor([float(value)], dtype=torch.float64, device=_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return t.item()
 
 
 def sum_over_ranks(value, device=None):
-    t = torch.tensor([float(value)], dtype=torch.float64, device=device or _device())
+    t = torch.tensor([float(value)], dtype=torch.float64, device=_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t.item()
 
 
 def gather_values(values, device=None):
     """All-gather a per-rank list of floats (equal lengths) -> flat list in rank order."""
-    t = torch.tensor(list(values), dtype=torch.float64, device=device or _device())
+    t = torch.tensor(list(values), dtype=torch.float64, device=_device(device))
     out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(out, t)
     return [v for o in out for v in o.tolist()]

@@ -38,8 +38,12 @@ def _worker(rank, world, port, n_items, q):
     padded = sums + [float("nan")] * (width - len(sums))
     allv = jdist.gather_values(padded)
     merged = [v for v in allv if v == v]
-    q.put((rank, start, count, jdist.max_over_ranks(max(errs)), merged,
-           jdist.sum_over_ranks(count)))
+    # bench.py passes its GPU to the reductions; under gloo (its shared-GPU rehearsal, and
+    # here, with no GPU at all) they must run on host tensors whatever device is named
+    import torch
+    gpu = torch.device("cuda", 0)
+    q.put((rank, start, count, jdist.max_over_ranks(max(errs), device=gpu), merged,
+           jdist.sum_over_ranks(count, device=gpu)))
     import torch.distributed as dist
     dist.destroy_process_group()
 
