@@ -5,6 +5,7 @@
 #include <cmath>
 #include <condition_variable>
 #include <deque>
+#include <exception>
 #include <thread>
 #include <cstdint>
 #include <cstdlib>
@@ -370,6 +371,22 @@ int check_where(int where) {
 // compute of k -- and synchronised before returning.
 constexpr size_t kSubDoubles = (size_t)16 << 20;  // 128 MiB of input + output per sub-batch
 
+// f's work behind the C-ABI: a C++ exception (a multi-GB host table that cannot be allocated,
+// a thread that cannot be started) becomes a status and an error text, never an unwind into
+// the caller (a JVM through JNI, ctypes)
+template <class F, class... A>
+int guarded(F& f, A... a) {
+  try {
+    return f(a...);
+  } catch (const std::bad_alloc&) {
+    return fail(JW_ERR_NO_MEMORY, "host memory exhausted (std::bad_alloc)");
+  } catch (const std::exception& e) {
+    return fail(JW_ERR_FAILURE, "C++ exception: %s", e.what());
+  } catch (...) {
+    return fail(JW_ERR_FAILURE, "unknown C++ exception");
+  }
+}
+
 template <class F>
 int run_items(int where, void* stream, const double* in, size_t in_per, double* out,
               size_t out_per, long items, F&& f) {
@@ -378,7 +395,7 @@ int run_items(int where, void* stream, const double* in, size_t in_per, double* 
   JW_HIP_TRY(hipGetDevice(&dev));
   note_device_used(dev);
   hipStream_t s = (hipStream_t)stream;
-  if (where == JW_DEVICE) return f(in, out, items, s);
+  if (where == JW_DEVICE) return guarded(f, in, out, items, s);
   HostStage* hs = nullptr;
   int st = host_stage(&hs);
   if (st != JW_OK) return st;
@@ -411,7 +428,7 @@ int run_items(int where, void* stream, const double* in, size_t in_per, double* 
       const int b = (int)(k & 1);
       JW_HIP_TRY(hipStreamWaitEvent(s, hs->loaded[b], 0));
       if (k >= 2) JW_HIP_TRY(hipStreamWaitEvent(s, hs->drained[b], 0));
-      int r = f(din[b], dout[b], count(k), s);
+      int r = guarded(f, (const double*)din[b], dout[b], count(k), s);
       if (r == JW_OK) JW_HIP_TRY(hipEventRecord(hs->done[b], s));
       return r;
     };

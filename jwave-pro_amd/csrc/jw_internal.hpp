@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <map>
 #include <mutex>
+#include <new>
 #include <shared_mutex>
 #include <string>
 #include <utility>
@@ -145,6 +146,9 @@ template <class Key, class Fill>
 int cached_table(DevCache<Key>& cache, const Key& key, size_t bytes, StreamAllocs& mem,
                  hipStream_t s, const void** out, Fill&& fill) {
   if ((*out = cache.find(key)) != nullptr) return JW_OK;
+  // tests: a host allocation failure in a table build (the C-ABI's exception guard,
+  // tests/test_jfft_limits_gpu.py)
+  if (const char* t = knob("JW_TEST_THROW_BADALLOC"); t && t[0] == '1') throw std::bad_alloc();
   // A table is kept for the process only while it fits the cache's budget AND a quarter of the
   // device memory that is free right now, so a co-resident framework that holds most of HBM is
   // not starved by tables the engine would keep after the call.
@@ -159,7 +163,14 @@ int cached_table(DevCache<Key>& cache, const Key& key, size_t bytes, StreamAlloc
   }
   void* p = nullptr;
   JW_HIP_TRY(hipMalloc(&p, bytes));
-  const int st = fill(p);
+  int st;
+  try {
+    st = fill(p);
+  } catch (...) {  // reported by the C-ABI's guard (run_items); the table is not kept
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(p);
+    throw;
+  }
   const hipError_t e = hipStreamSynchronize(s);  // complete before another thread may read it
   if (st != JW_OK || e != hipSuccess) {
     (void)hipFree(p);

@@ -60,11 +60,19 @@ void java_twiddles(long n, bool inverse, const Put& put) {
     java_stages(0, lg, inverse, put);
     return;
   }
-  std::thread top([&] { java_stages(lg - 1, lg, inverse, put); });
-  std::thread next([&] { java_stages(lg - 2, lg - 1, inverse, put); });
+  // a thread that cannot be started (std::system_error) leaves its stage to this one: nothing
+  // may throw across the C-ABI
+  std::thread top, next;
+  try {
+    top = std::thread([&] { java_stages(lg - 1, lg, inverse, put); });
+    next = std::thread([&] { java_stages(lg - 2, lg - 1, inverse, put); });
+  } catch (...) {
+  }
   java_stages(0, lg - 2, inverse, put);
-  top.join();
-  next.join();
+  if (!next.joinable()) java_stages(lg - 2, lg - 1, inverse, put);
+  if (!top.joinable()) java_stages(lg - 1, lg, inverse, put);
+  if (top.joinable()) top.join();
+  if (next.joinable()) next.join();
 }
 
 cplx* host_table(size_t entries) {

@@ -67,8 +67,13 @@ int bs_tables(long n, bool inverse, BsTab* out, StreamAllocs& mem, hipStream_t s
         };
         const int nt = n >= (1L << 16) ? host_threads() : 1;
         std::vector<std::thread> pool;
-        for (int t = 1; t < nt; ++t) pool.emplace_back(fill, n * t / nt, n * (t + 1) / nt);
+        try {  // slices whose thread cannot be started run here: nothing throws across the C-ABI
+          pool.reserve(nt);
+          for (int t = 1; t < nt; ++t) pool.emplace_back(fill, n * t / nt, n * (t + 1) / nt);
+        } catch (...) {
+        }
         fill(0, n / nt);
+        for (int t = (int)pool.size() + 1; t < nt; ++t) fill(n * t / nt, n * (t + 1) / nt);
         for (auto& th : pool) th.join();
         b[0] = make_double2(chirp[0].x, -chirp[0].y);  // :285-290, conjugate() = (r, -j)
         for (long i = 1; i < n; ++i) {

@@ -106,3 +106,21 @@ def test_modwt_fft_method_at_2_29(device):
     torch.cuda.synchronize()
     err = (torch.linalg.vector_norm(c - d) / torch.linalg.vector_norm(d)).item()
     assert err < 1e-6, err
+
+
+def test_host_allocation_failure_is_a_status(knobs, device):
+    # a C++ exception inside the engine (here std::bad_alloc from a twiddle-table build, injected
+    # by JW_TEST_THROW_BADALLOC) comes back as JW_ERR_NO_MEMORY with a message -- never an unwind
+    # into the caller -- and the table is not kept: the same call succeeds afterwards, bit-exact
+    import torch
+    n = 3 << 11  # not a power of two: Bluestein over m = 8192 (a table no other test builds first)
+    z = torch.rand((n, 2), dtype=torch.float64, device=device)
+    out = torch.empty_like(z)
+    knobs.setenv("JW_TEST_THROW_BADALLOC", "1")
+    st = _native.lib().jw_fft_forward_ex(_p(z), _p(out), n, 1, _native.JW_ARITH_STRICT,
+                                         _native.JW_DEVICE, None)
+    assert st == _native.JW_ERR_NO_MEMORY and "bad_alloc" in _native.last_error()
+    knobs.delenv("JW_TEST_THROW_BADALLOC")
+    X = fft(z, n, 1, False)
+    ref = orc.fft(torch.view_as_complex(z).cpu().numpy())
+    assert torch.equal(bits(X.cpu()), bits(torch.view_as_real(torch.from_numpy(ref))))
