@@ -657,7 +657,7 @@ static bool auto_level_fft(long n, int L, int j, int threshold) {
 //   JW_ARITH_FMA (fast contract): FFT runs the exact-twiddle frequency-domain pyramid; AUTO and
 //     DIRECT run the direct kernels, which are faster and more accurate than any FFT path here.
 //   A level the reference would run through its FFT at a length the FFT paths do not take
-//     (STRICT: powers of two past 2^28, other n past 2^23; FMA's pyramid: n past 2^23) is
+//     (STRICT: powers of two past 2^30, other n past 2^29; FMA's pyramid: n past 2^23) is
 //     JW_ERR_UNSUPPORTED with the limit in the message -- never a silent switch to DIRECT, whose
 //     values differ from the JVM's FFT path by up to ~1e-10.
 enum class ModwtPath { kDirect, kStrictLevels, kPyramid, kUnsupported };
