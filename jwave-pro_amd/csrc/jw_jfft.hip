@@ -277,8 +277,8 @@ int forward_lines(const ModwtPlan& p, const bool* fft, const cplx* F, const Tw& 
     if (fft[j]) {
       st = with_lc(N, [&](auto LCc) -> int {
         constexpr int LC = decltype(LCc)::value;
-        return launch_grid<LC>(kline_modwt<LC, 1, 2, LineIn, LineFwdMid, LineOut>,
-                               (c.nb + Geo<LC>::T - 1) / Geo<LC>::T, s, LineIn{vin, vs, vin, vs},
+        return launch_grid<LC, kLineEPT<LC>>(kline_modwt<LC, 1, 2, LineIn, LineFwdMid, LineOut>,
+                               (c.nb + LineGeo<LC>::T - 1) / LineGeo<LC>::T, s, LineIn{vin, vs, vin, vs},
                                LineFwdMid{spec_h(F, N, j), spec_g(F, N, j)},
                                LineOut{w, rs, vout, vos}, c.nb, twf.p1, twi.p1, 1.0 / (double)N);
       });
@@ -304,8 +304,8 @@ int inverse_lines(const ModwtPlan& p, const bool* fft, const cplx* F, const Tw& 
     if (fft[j]) {
       st = with_lc(N, [&](auto LCc) -> int {
         constexpr int LC = decltype(LCc)::value;
-        return launch_grid<LC>(kline_modwt<LC, 2, 1, LineIn, LineAdjMid, LineOut>,
-                               (c.nb + Geo<LC>::T - 1) / Geo<LC>::T, s, LineIn{vin, vs, w, rs},
+        return launch_grid<LC, kLineEPT<LC>>(kline_modwt<LC, 2, 1, LineIn, LineAdjMid, LineOut>,
+                               (c.nb + LineGeo<LC>::T - 1) / LineGeo<LC>::T, s, LineIn{vin, vs, w, rs},
                                LineAdjMid{spec_g(F, N, j), spec_h(F, N, j)},
                                LineOut{vout, N, vout, N}, c.nb, twf.p1, twi.p1, 1.0 / (double)N);
       });

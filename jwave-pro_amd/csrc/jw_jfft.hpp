@@ -49,18 +49,28 @@ __host__ __device__ constexpr int ilog2(long v) {
 #ifndef JF_EPT1024
 #define JF_EPT1024 8
 #endif
+// Points per thread of the 2048- and 4096-point COLUMNS (kp1 / kp2s / kp2p / kp2r).  16: 4 and 2
+// columns per workgroup (64- and 32-byte pieces) at 131 KB of LDS, one workgroup per CU; 8 (the
+// whole-line kernels keep it, LineGeo): 2 and 1 columns (32- and 16-byte pieces), two per CU.
+// JWave's FFT at 2^21 / 2^22: 2.89 -> 2.43 / 3.91 -> 2.97 ms per 128 Mi points; AUTO db4 J=8
+// 1,516 -> 1,535 Msamples/s (profiles/r06/ab/ept_big/).  A/B builds: JF_EPT_BIG=8.
+#ifndef JF_EPT_BIG
+#define JF_EPT_BIG 16
+#endif
 #ifndef JF_SWZ  // LDS layout of a column (A/B builds: 0 = one pad slot per 8 points)
 #define JF_SWZ 1
 #endif
 #ifndef JF_SWZ_MIN  // shortest column that takes the swizzle (A/B builds)
 #define JF_SWZ_MIN 1024
 #endif
-template <int LC>
+// EPTO: the points per thread when given (the whole-line kernels' LineGeo), else the column rule
+template <int LC, int EPTO = 0>
 struct Geo {
   static constexpr int LOG = ilog2(LC);
-  // (a 4096-point column needs 16 per thread: at most kNT threads per column)
-  static constexpr int EPT = LC == 1024 ? JF_EPT1024
-                                        : (LC < kEPT ? LC : (LC / kNT > kEPT ? LC / kNT : kEPT));
+  static constexpr int EPT = EPTO       ? EPTO
+                             : LC == 1024 ? JF_EPT1024
+                             : LC >= 2048 ? JF_EPT_BIG
+                                          : (LC < kEPT ? LC : kEPT);
   static constexpr int GMAX = ilog2(EPT);
   static constexpr int TPC = LC / EPT;  // threads per column (divides 64 when <= 64)
   static constexpr int T = kNT / TPC;   // columns per workgroup
@@ -72,6 +82,12 @@ struct Geo {
   static constexpr int CS = SWZ ? LC + 6 : LC + LC / 8 + (LC == 1024 ? 3 : LC == 2048 ? 5 : 1);
   static constexpr size_t LDS_BYTES = (size_t)T * CS * sizeof(cplx);
 };
+// the whole-line kernels (kline_*): 8 points per thread at every length (16 at 2048 / 4096 points
+// would spill their NIN / NOUT streams)
+template <int LC>
+constexpr int kLineEPT = LC >= 2048 ? 8 : 0;
+template <int LC>
+using LineGeo = Geo<LC, kLineEPT<LC>>;
 
 // LDS slot of column position pos.  Columns of >= 1024 points: the low three bits XORed with bits
 // 3-5, 6-8 and 9-11 (a permutation inside each group of 8 slots), which spreads the strided
@@ -104,9 +120,9 @@ __device__ __forceinline__ void bfly(cplx& u, cplx& v, cplx w) {
   v = make_double2(a.x - t.x, a.y - t.y);
 }
 
-template <int LC>
+template <int LC, int EO = 0>
 __device__ __forceinline__ void col_sync() {
-  if constexpr (Geo<LC>::TPC <= 64) {
+  if constexpr (Geo<LC, EO>::TPC <= 64) {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -118,11 +134,11 @@ __device__ __forceinline__ void col_sync() {
 // The butterflies of stages t0 .. t0+G-1 on a thread's NSET = EPT / 2^G sets held in v (set i:
 // positions base[i] + (m << t0), m < 2^G, at v[i 2^G + m]); stage t pairs j, j + 2^t with bit t
 // clear and uses tw[2^t + (j mod 2^t)].
-template <int LC, int G>
-__device__ __forceinline__ void stage_math(cplx (&v)[Geo<LC>::EPT],
-                                           const int (&base)[Geo<LC>::EPT >> G], int t0,
+template <int LC, int G, int EO = 0>
+__device__ __forceinline__ void stage_math(cplx (&v)[(Geo<LC, EO>::EPT)],
+                                           const int (&base)[(Geo<LC, EO>::EPT >> G)], int t0,
                                            const cplx* __restrict__ tw) {
-  using Gm = Geo<LC>;
+  using Gm = Geo<LC, EO>;
   constexpr int E = 1 << G, NSET = Gm::EPT / E;
   const int lowmask = (1 << t0) - 1;
 #pragma unroll
@@ -150,10 +166,10 @@ __device__ __forceinline__ int set_base(int set, int t0, int G) {
 
 // Stages t0 .. t0+G-1 of one column (positions j; stage t pairs j, j + 2^t with bit t clear and
 // uses tw[2^t + (j mod 2^t)]).  Thread tl owns EPT/2^G sets {base + m 2^t0 : m < 2^G}.
-template <int LC, int G>
+template <int LC, int G, int EO = 0>
 __device__ __forceinline__ void stage_group(cplx* __restrict__ col, int tl, int t0,
                                             const cplx* __restrict__ tw) {
-  using Gm = Geo<LC>;
+  using Gm = Geo<LC, EO>;
   constexpr int E = 1 << G, NSET = Gm::EPT / E;
   cplx v[Gm::EPT];
   int base[NSET];
@@ -163,7 +179,7 @@ __device__ __forceinline__ void stage_group(cplx* __restrict__ col, int tl, int 
 #pragma unroll
     for (int m = 0; m < E; ++m) v[i * E + m] = col[pidx<LC>(base[i] + (m << t0))];
   }
-  stage_math<LC, G>(v, base, t0, tw);
+  stage_math<LC, G, EO>(v, base, t0, tw);
 #pragma unroll
   for (int i = 0; i < NSET; ++i) {
 #pragma unroll
@@ -173,22 +189,22 @@ __device__ __forceinline__ void stage_group(cplx* __restrict__ col, int tl, int 
 
 // all LOG stages of one column, in groups of GMAX (the column's points must be in place);
 // stages T0 .. TEND - 1 only when TEND is given (a multiple of GMAX past T0)
-template <int LC, int T0 = 0, int TEND = Geo<LC>::LOG>
+template <int LC, int T0 = 0, int TEND = Geo<LC>::LOG, int EO = 0>
 __device__ __forceinline__ void run_stages(cplx* __restrict__ col, int tl,
                                            const cplx* __restrict__ tw) {
-  using Gm = Geo<LC>;
+  using Gm = Geo<LC, EO>;
   if constexpr (T0 < TEND) {
     constexpr int G = (TEND - T0) < Gm::GMAX ? (TEND - T0) : Gm::GMAX;
-    if constexpr (T0 > 0) col_sync<LC>();
-    stage_group<LC, G>(col, tl, T0, tw);
-    run_stages<LC, T0 + G, TEND>(col, tl, tw);
+    if constexpr (T0 > 0) col_sync<LC, EO>();
+    stage_group<LC, G, EO>(col, tl, T0, tw);
+    run_stages<LC, T0 + G, TEND, EO>(col, tl, tw);
   }
 }
 
 // the thread's own points of its column: positions tl + TPC k
-template <int LC>
+template <int LC, int EO = 0>
 __device__ __forceinline__ int own_pos(int tl, int k) {
-  return tl + Geo<LC>::TPC * k;
+  return tl + Geo<LC, EO>::TPC * k;
 }
 
 // Workgroup -> (column tile, item).  When the tiles split evenly over the 8 XCDs, every XCD
@@ -309,8 +325,11 @@ __global__ __launch_bounds__(kNT) void kp2s(In in, Out out, int wbits, long nite
 // pass 2, then NF pointwise products (Mid: cplx operator()(int f, long item, long i, cplx X),
 // i = the natural index h W + l), each run through pass 1 of the next transform (table tw1)
 // and stored as rows (Out: operator()(int f, long item, long j, cplx v), j = row LC + pos).
+// (a workgroup of more than 80 KB of LDS is alone on its CU: two waves per SIMD, registers to match)
+template <int LC>
+constexpr int kColWPE = Geo<LC>::LDS_BYTES > 80 * 1024 ? 2 : JF_KP2R_WPE;
 template <int LC, int NF, class In, class Mid, class Out>
-__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(NF == 1 ? JF_KP2R_WPE
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(NF == 1 ? kColWPE<LC>
                                                                              : 1))) void kp2p(
     In in, Mid mid, Out out, int wbits, long nitems,
                                             const cplx* __restrict__ tw2,
@@ -365,7 +384,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(NF == 1 ? J
 // with no spill (the unfused one spilled 20, so it keeps its own allocation)
 template <int LC, int NIN, bool FUSE, class In, class Post, class Out>
 __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(
-    NIN == 1 || FUSE ? JF_KP2R_WPE : 1))) void kp2r(
+    NIN == 1 || FUSE ? kColWPE<LC> : 1))) void kp2r(
     In in, Post post, Out out, int wbits, long nitems,
                                             const cplx* __restrict__ tw2,
                                             const cplx* __restrict__ tw1f) {
@@ -424,12 +443,13 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(
 // load line `line` (In: cplx operator()(long line, int r)) bit-reversed into col
 template <int LC, class In>
 __device__ __forceinline__ void line_load_rev(cplx* col, int tl, const In& in, long line) {
-  using G = Geo<LC>;
+  using G = LineGeo<LC>;
+  constexpr int E = kLineEPT<LC>;
   cplx v[G::EPT];
 #pragma unroll
-  for (int k = 0; k < G::EPT; ++k) v[k] = in(line, own_pos<LC>(tl, k));
+  for (int k = 0; k < G::EPT; ++k) v[k] = in(line, own_pos<LC, E>(tl, k));
 #pragma unroll
-  for (int k = 0; k < G::EPT; ++k) col[pidx<LC>(brev(own_pos<LC>(tl, k), G::LOG))] = v[k];
+  for (int k = 0; k < G::EPT; ++k) col[pidx<LC>(brev(own_pos<LC, E>(tl, k), G::LOG))] = v[k];
 }
 
 // jw_fft (JW_ARITH_STRICT): In (line, r) -> cplx; Out (line, r, cplx); scale applied to both
@@ -438,7 +458,8 @@ template <int LC, class In, class Out>
 __global__ __launch_bounds__(kNT) void kline_fft(In in, Out out, long nlines,
                                                  const cplx* __restrict__ tw, double scale,
                                                  int do_scale) {
-  using G = Geo<LC>;
+  using G = LineGeo<LC>;
+  constexpr int E = kLineEPT<LC>;
   extern __shared__ cplx lds[];
   const int cc = threadIdx.x / G::TPC, tl = threadIdx.x % G::TPC;
   const long line = (long)blockIdx.x * G::T + cc;
@@ -446,13 +467,13 @@ __global__ __launch_bounds__(kNT) void kline_fft(In in, Out out, long nlines,
   cplx* col = lds + cc * G::CS;
   line_load_rev<LC>(col, tl, [&](long ln, int r) { return valid ? in(ln, r) : cplx{0.0, 0.0}; },
                     line);
-  col_sync<LC>();
-  run_stages<LC>(col, tl, tw);
-  col_sync<LC>();
+  col_sync<LC, E>();
+  run_stages<LC, 0, G::LOG, E>(col, tl, tw);
+  col_sync<LC, E>();
   if (!valid) return;
 #pragma unroll
   for (int k = 0; k < G::EPT; ++k) {
-    const int p = own_pos<LC>(tl, k);
+    const int p = own_pos<LC, E>(tl, k);
     cplx v = col[pidx<LC>(p)];
     if (do_scale) v = jscale(v, scale);
     out(line, p, v);
@@ -472,7 +493,8 @@ __global__ __launch_bounds__(kNT) void kline_modwt(In in, Mid mid, Out out, long
                                                    const cplx* __restrict__ twf,
                                                    const cplx* __restrict__ twi, double inv_n) {
   static_assert(NIN == 1 || NOUT == 1, "forward: 1 in / 2 out; inverse: 2 in / 1 out");
-  using G = Geo<LC>;
+  using G = LineGeo<LC>;
+  constexpr int E = kLineEPT<LC>;
   extern __shared__ cplx lds[];
   const int cc = threadIdx.x / G::TPC, tl = threadIdx.x % G::TPC;
   const long line = (long)blockIdx.x * G::T + cc;
@@ -481,30 +503,30 @@ __global__ __launch_bounds__(kNT) void kline_modwt(In in, Mid mid, Out out, long
   double acc[G::EPT];
 #pragma unroll
   for (int s = 0; s < NIN; ++s) {
-    if (s > 0) col_sync<LC>();
+    if (s > 0) col_sync<LC, E>();
     line_load_rev<LC>(
         col, tl,
         [&](long ln, int r) { return make_double2(valid ? in(s, ln, r) : 0.0, 0.0); }, line);
-    col_sync<LC>();
-    run_stages<LC>(col, tl, twf);
-    col_sync<LC>();
+    col_sync<LC, E>();
+    run_stages<LC, 0, G::LOG, E>(col, tl, twf);
+    col_sync<LC, E>();
     cplx X[G::EPT];
 #pragma unroll
-    for (int k = 0; k < G::EPT; ++k) X[k] = col[pidx<LC>(own_pos<LC>(tl, k))];
+    for (int k = 0; k < G::EPT; ++k) X[k] = col[pidx<LC>(own_pos<LC, E>(tl, k))];
 #pragma unroll
     for (int f = 0; f < NOUT; ++f) {
-      col_sync<LC>();
+      col_sync<LC, E>();
 #pragma unroll
       for (int k = 0; k < G::EPT; ++k) {
-        const int p = own_pos<LC>(tl, k);
+        const int p = own_pos<LC, E>(tl, k);
         col[pidx<LC>(brev(p, G::LOG))] = mid(s, f, p, X[k]);
       }
-      col_sync<LC>();
-      run_stages<LC>(col, tl, twi);
-      col_sync<LC>();
+      col_sync<LC, E>();
+      run_stages<LC, 0, G::LOG, E>(col, tl, twi);
+      col_sync<LC, E>();
 #pragma unroll
       for (int k = 0; k < G::EPT; ++k) {
-        const int p = own_pos<LC>(tl, k);
+        const int p = own_pos<LC, E>(tl, k);
         const double v = col[pidx<LC>(p)].x * inv_n;  // result[i].mul(1.0/n).getReal()
         if constexpr (NOUT == 2) {
           if (valid) out(f, line, p, v);
@@ -517,7 +539,7 @@ __global__ __launch_bounds__(kNT) void kline_modwt(In in, Mid mid, Out out, long
   if constexpr (NOUT == 1) {
     if (valid) {
 #pragma unroll
-      for (int k = 0; k < G::EPT; ++k) out(0, line, own_pos<LC>(tl, k), acc[k]);
+      for (int k = 0; k < G::EPT; ++k) out(0, line, own_pos<LC, E>(tl, k), acc[k]);
     }
   }
 }
@@ -719,7 +741,8 @@ __global__ __launch_bounds__(kNT) void kline_conv(In in, Out out, long nlines,
                                                   const cplx* __restrict__ B,
                                                   const cplx* __restrict__ twf,
                                                   const cplx* __restrict__ twi) {
-  using G = Geo<LC>;
+  using G = LineGeo<LC>;
+  constexpr int E = kLineEPT<LC>;
   extern __shared__ cplx lds[];
   const int cc = threadIdx.x / G::TPC, tl = threadIdx.x % G::TPC;
   const long line = (long)blockIdx.x * G::T + cc;
@@ -727,25 +750,25 @@ __global__ __launch_bounds__(kNT) void kline_conv(In in, Out out, long nlines,
   cplx* col = lds + cc * G::CS;
   line_load_rev<LC>(col, tl, [&](long ln, int r) { return valid ? in(ln, r) : cplx{0.0, 0.0}; },
                     line);
-  col_sync<LC>();
-  run_stages<LC>(col, tl, twf);
-  col_sync<LC>();
+  col_sync<LC, E>();
+  run_stages<LC, 0, G::LOG, E>(col, tl, twf);
+  col_sync<LC, E>();
   cplx X[G::EPT];
 #pragma unroll
-  for (int k = 0; k < G::EPT; ++k) X[k] = col[pidx<LC>(own_pos<LC>(tl, k))];
-  col_sync<LC>();
+  for (int k = 0; k < G::EPT; ++k) X[k] = col[pidx<LC>(own_pos<LC, E>(tl, k))];
+  col_sync<LC, E>();
 #pragma unroll
   for (int k = 0; k < G::EPT; ++k) {
-    const int p = own_pos<LC>(tl, k);
+    const int p = own_pos<LC, E>(tl, k);
     col[pidx<LC>(brev(p, G::LOG))] = jmul(X[k], B[p]);
   }
-  col_sync<LC>();
-  run_stages<LC>(col, tl, twi);
-  col_sync<LC>();
+  col_sync<LC, E>();
+  run_stages<LC, 0, G::LOG, E>(col, tl, twi);
+  col_sync<LC, E>();
   if (!valid) return;
 #pragma unroll
   for (int k = 0; k < G::EPT; ++k) {
-    const int p = own_pos<LC>(tl, k);
+    const int p = own_pos<LC, E>(tl, k);
     out(line, p, col[pidx<LC>(p)]);
   }
 }

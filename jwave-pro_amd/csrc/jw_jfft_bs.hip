@@ -252,7 +252,8 @@ int bs_rows(long n, bool inverse, long items, Pre pre, Post post, StreamAllocs& 
     if ((st = twiddles(m, true, (int)m, &twi, mem, s)) != JW_OK) return st;
     return with_lc(m, [&](auto LCc) -> int {
       constexpr int LC = decltype(LCc)::value;
-      return launch_grid<LC>(kline_conv<LC, Pre, Post>, (items + Geo<LC>::T - 1) / Geo<LC>::T, s,
+      return launch_grid<LC, kLineEPT<LC>>(kline_conv<LC, Pre, Post>,
+                                           (items + LineGeo<LC>::T - 1) / LineGeo<LC>::T, s,
                              pre, post, items, T.B, twf.p1, twi.p1);
     });
   }

@@ -28,6 +28,13 @@ inline int split_lc1(long n) { return n <= kLineMax ? (int)n : 1 << (ilog2(n) / 
 // default; env JW_JFFT_3PASS_MIN (a power of two >= 2^18) lowers it, so the tests can check the
 // three-pass code against the oracle at sizes the oracle finishes quickly.
 long three_pass_min();
+// Plain transforms (jw_fft STRICT, filter spectra, Bluestein's b) switch earlier: from 2^23 the
+// three-pass split (columns of 2^11..2^12 x 2^6 x 2^6) beats the two 2^11..2^12-point column
+// passes: 4.43 -> 3.18 ms at 2^23, 4.82 -> 3.54 ms at 2^24 per 128 Mi points, equal at 2^22
+// (profiles/r06/ab/ept_big/fft3.txt).  MODWT's fused levels and Bluestein's fused convolution
+// stay two-pass up to three_pass_min(): unfused three passes measured slower there (AUTO db4 J=4
+// at 2^22: 1,922 vs 1,273 Msamples/s; Bluestein m = 2^23: 2.73 vs 3.19 ms).
+inline long plain_three_pass_min() { return std::min(three_pass_min(), 1L << 23); }
 constexpr long kStrictPow2Max = kStrictFftPow2Max;  // the longest power-of-two STRICT transform
 // bits of A, B, C for a three-pass n = 2^lg (18 <= lg <= 36)
 inline void split3(int lg, int* a, int* b, int* c) {
@@ -79,9 +86,9 @@ inline int with_big_lc(long lc, F&& f) {
 }
 #undef JF_CASE
 
-template <int LC, class K, class... A>
+template <int LC, int E = 0, class K, class... A>
 int launch_grid(K kern, long blocks, hipStream_t s, A... args) {
-  const size_t lds = Geo<LC>::LDS_BYTES;
+  const size_t lds = Geo<LC, E>::LDS_BYTES;
   JW_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)lds));
   if (blocks <= 0) return JW_OK;
@@ -336,7 +343,8 @@ inline int fft_rows3(long n, bool inverse, long items, In in, Out out, StreamAll
 template <class In, class Out = OutCS>
 inline int fft_rows(long n, bool inverse, long items, In in, Out out, StreamAllocs& mem,
              hipStream_t s) {
-  if (n > kLineMax && n >= three_pass_min()) return fft_rows3(n, inverse, items, in, out, mem, s);
+  if (n > kLineMax && n >= plain_three_pass_min())
+    return fft_rows3(n, inverse, items, in, out, mem, s);
   const int lc1 = split_lc1(n);
   Tw tw;
   int st = twiddles(n, inverse, lc1, &tw, mem, s);
@@ -344,7 +352,8 @@ inline int fft_rows(long n, bool inverse, long items, In in, Out out, StreamAllo
   if (n <= kLineMax) {
     return with_lc(n, [&](auto LCc) -> int {
       constexpr int LC = decltype(LCc)::value;
-      return launch_grid<LC>(kline_fft<LC, In, Out>, (items + Geo<LC>::T - 1) / Geo<LC>::T, s,
+      return launch_grid<LC, kLineEPT<LC>>(kline_fft<LC, In, Out>,
+                                           (items + LineGeo<LC>::T - 1) / LineGeo<LC>::T, s,
                              in, out, items, tw.p1, 1.0, 0);
     });
   }

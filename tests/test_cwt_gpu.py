@@ -428,3 +428,40 @@ def test_split_coarse_path_bit_identical(knobs):
     knobs.setenv("JW_CWT_SPLIT", "1")
     got = t.transformFFTBatch(torch.from_numpy(xs).cuda(), scales, 1.0).cpu().numpy()
     assert np.array_equal(got, base)
+
+
+def test_reference_cwt_test_params_fixture():
+    # the reference's own CWT test parameters (scripts/generate_basic_reference.py:120-130 ->
+    # testdata/cwt_test_params.txt: fs = 1000, 256 samples, 20 scales 1 .. 50), run through both
+    # CWT paths on its clean test signal: transformFFT against the oracle (exact twiddles 1e-12,
+    # JWave's recurrence 1e-10, normwise), the direct transform bit for bit, for the wavelets
+    # ContinuousWaveletTransformTest.java uses (Morlet(1, 1) :48, MexicanHat(1) :72, Paul(4) :281,
+    # Meyer :301), linear and log scales
+    import os
+    from _util import GOLDEN, clean_signal
+    p = {}
+    with open(os.path.join(GOLDEN, "reference_testdata", "cwt_test_params.txt")) as f:
+        for line in f:
+            line = line.strip()
+            if line and not line.startswith("#"):
+                k, v = line.split("=")
+                p[k] = float(v)
+    fs, n, ns = p["sampling_rate"], int(p["signal_length"]), int(p["num_scales"])
+    x = clean_signal(n)
+    for scales in (CWT.generateLinearScales(p["scale_min"], p["scale_max"], ns),
+                   CWT.generateLogScales(p["scale_min"], p["scale_max"], ns)):
+        for wv, kind, params in ((MorletWavelet(1.0, 1.0), "morlet", (1.0, 1.0)),
+                                 (MexicanHatWavelet(1.0), "mexhat", (1.0, 0.0)),
+                                 (PaulWavelet(4), "paul", (4.0,)), (MeyerWavelet(), "meyer", ())):
+            got = CWT(wv).transformFFT(x, scales, fs).getCoefficients()
+            ex = orc.cwt_fft(x, scales, fs, kind, params, int(PaddingType.SYMMETRIC), exact=True)
+            jw = orc.cwt_fft(x, scales, fs, kind, params, int(PaddingType.SYMMETRIC), exact=False)
+            assert got.shape == (ns, n)
+            if np.max(np.abs(ex)) == 0:  # Meyer at fs = 1000: its band misses every bin, all zeros
+                assert np.max(np.abs(jw)) == 0 and not np.any(got), kind
+            else:
+                assert nw(got, ex) < TOL_EXACT and nw(got, jw) < TOL_JWAVE, (kind, nw(got, ex), nw(got, jw))
+            d = CWT(wv).transform(x, scales, fs).getCoefficients()
+            ref = orc.cwt_direct(x, kind, wv.params(), scales, fs)
+            assert np.array_equal(d.real.view(np.uint64), ref.real.view(np.uint64))
+            assert np.array_equal(d.imag.view(np.uint64), ref.imag.view(np.uint64))

@@ -114,8 +114,10 @@ def test_auto_full_size(wname, J, device):
     assert (xr - x).abs().max().item() < 1e-8
 
 
+# (2^21, 2^22: two passes over 2048-point columns, 4 per workgroup; 2^23: three passes, the
+# plain-transform split)
 POW2 = [2, 4, 8, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 1 << 14, 1 << 15, 1 << 16,
-        1 << 17, 1 << 18, 1 << 19, 1 << 20, 1 << 21]
+        1 << 17, 1 << 18, 1 << 19, 1 << 20, 1 << 21, 1 << 22, 1 << 23]
 
 
 @pytest.mark.parametrize("n", POW2)
@@ -151,9 +153,15 @@ def test_fft_strict_in_place_and_device(device):
 
 
 def test_fft_strict_largest_column():
-    # 2^24 = 4096 x 4096: the 4096-point column kernels (the chirp-z size of n up to 2^23)
+    # the 4096-point column kernels: pass 1 of 2^24 (three passes for plain transforms from 2^23,
+    # jw_jfft_host.hpp plain_three_pass_min) and the two-pass chirp-z convolution of n = 2^23 - 1
+    # (m = 2^24 = 4096 x 4096: kp1 / kp2p / kp2s on 4096-point columns, 2 per workgroup)
     n = 1 << 24
     rng = np.random.default_rng(24)
+    z = rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n)
+    X = FastFourierTransform().forwardComplex(z)
+    assert bits_equal(X.view(np.float64), orc.fft(z).view(np.float64))
+    n = (1 << 23) - 1
     z = rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n)
     X = FastFourierTransform().forwardComplex(z)
     assert bits_equal(X.view(np.float64), orc.fft(z).view(np.float64))

@@ -44,7 +44,10 @@ for _ in range(a.reps):
 e1.record(s)
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / a.reps
-passes = 3 if a.n >= int(os.environ.get("JW_JFFT_3PASS_MIN", 1 << 25)) else 2
+# plain transforms: three passes from min(JW_JFFT_3PASS_MIN or 2^25, 2^23) (jw_jfft_host.hpp
+# plain_three_pass_min); Bluestein lengths report their m-point convolution's two passes
+pow2 = a.n & (a.n - 1) == 0
+passes = 3 if pow2 and a.n >= min(int(os.environ.get("JW_JFFT_3PASS_MIN", 1 << 25)), 1 << 23) else 2
 pass_bytes = 32 * a.n * a.batch  # one pass reads and writes every complex point once
 print(json.dumps({"n": a.n, "batch": a.batch, "passes": passes, "ms": round(ms, 3),
                   "pass_bytes": pass_bytes,
