@@ -33,7 +33,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "modwt_pmc_traffic.json")
 # cwt / fwt2d HBM bytes per step at their default configs (tools/evidence.sh TAG traffic W,
 # tools/summarize.py traffic)
-TRAFFIC_STEP_FILE = os.path.join(ROOT, "profiles", "r05", "traffic_cwt_fwt2d.json")
+TRAFFIC_STEP_FILE = os.path.join(ROOT, "profiles", "r06", "traffic_step.json")
 
 
 def generate_inputs(gen, min_seconds=1.0):
