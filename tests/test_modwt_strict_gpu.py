@@ -310,6 +310,21 @@ def test_fft_strict_three_pass_default_geometry(lg):
     assert bits_equal(X.view(np.float64), orc.fft(z).view(np.float64))
 
 
+def test_auto_2_23_fused_columns_bit_exact():
+    # JWave's default path at 2^23: the fused two-pass levels on 2048 x 4096 columns (kp2p / kp2r
+    # on 4096-point columns, 2 per workgroup) and filter spectra through the plain three-pass
+    # transform (jw_jfft_host.hpp plain_three_pass_min), forward and inverse
+    n = 1 << 23
+    wv = W.Daubechies4()
+    g, h = ofilters(wv)
+    x = orc.fill_uniform(n, 23)
+    m = MODWTTransform(wv)
+    c = m.forwardMODWT(x[None, :], 1)
+    ref = orc.modwt_forward(x, 1, g, h, "auto")
+    assert bits_equal(c[0], ref)
+    assert bits_equal(m.inverseMODWT(c)[0], orc.modwt_inverse(ref, g, h, "auto"))
+
+
 def test_auto_2_25_forward_bit_exact():
     # JWave's default path at a length past the two-pass FFT: db4 level 1 through the
     # unfused long-line MODWT (jw_jfft.hip modwt_strict_long) on three-pass transforms
