@@ -127,7 +127,8 @@ int jw_modwt_plan_filters(const jw_modwt_plan* plan, double* g, double* h);
  * twiddles for powers of two (FastFourierTransform.java:172-212) and its Bluestein transform for
  * other lengths (:259-324), both bit-identical to the JVM over the reference's own domain:
  * power-of-two n <= 2^30 and other n <= 2^29 (Bluestein's m <= 2^30; past that the reference's
- * int arithmetic overflows), transforms longer than 2^24 points in three column passes -- given that the
+ * int arithmetic overflows), the longest transforms in three column passes (the levels from 2^25,
+ * jw_fft_*_ex from 2^23: the split changes access shapes, not one operation) -- given that the
  * JVM's Math.sin/Math.cos are correctly rounded at the twiddle and chirp angles (Java specifies
  * them to 1 ulp; the engine and the oracle both take the correctly rounded value).
  * With a JW_ARITH_FMA plan (the fast contract) FFT runs the exact-twiddle frequency-domain
