@@ -88,6 +88,17 @@ template <int LC>
 constexpr int kLineEPT = LC >= 2048 ? 8 : 0;
 template <int LC>
 using LineGeo = Geo<LC, kLineEPT<LC>>;
+// the plain transforms' column passes (fft_rows / fft_rows3: kp1 and kp2s alone) take 16 points
+// per thread at 1024 points too (8 columns, 128-byte pieces, one workgroup per CU): JWave's FFT
+// at 2^20 2.30 -> 2.14 ms per 128 Mi points (profiles/r06/ab/ept_big/fft_ept1024_16.txt); the
+// fused MODWT kernels keep 8 there (AUTO's forward kp2p<1024> wants two workgroups per CU)
+#ifndef JF_PLAIN_EPT1024
+#define JF_PLAIN_EPT1024 16
+#endif
+template <int LC>
+constexpr int kPlainEPT = LC == 1024 ? JF_PLAIN_EPT1024 : 0;
+template <int LC>
+using PlainGeo = Geo<LC, kPlainEPT<LC>>;
 
 // LDS slot of column position pos.  Columns of >= 1024 points: the low three bits XORed with bits
 // 3-5, 6-8 and 9-11 (a permutation inside each group of 8 slots), which spreads the strided
@@ -239,9 +250,9 @@ __device__ __forceinline__ void tile_item(int ntiles, long nitems, int* tile, lo
 // (W = 2^wbits columns); outputs are operator()(long item, long i, cplx v), where a row store
 // (Z, the pass-1 result) writes i = row LC + pos, row = rev(column).
 // ---------------------------------------------------------------------------------------
-template <int LC, bool REV, class In>
+template <int LC, bool REV, class In, int EO = 0>
 __device__ __forceinline__ void load_cols(cplx* lds, const In& in, long item, int c0, int wbits) {
-  using G = Geo<LC>;
+  using G = Geo<LC, EO>;
   cplx v[G::EPT];
 #pragma unroll
   for (int k = 0; k < G::EPT; ++k) {
@@ -256,10 +267,10 @@ __device__ __forceinline__ void load_cols(cplx* lds, const In& in, long item, in
   }
 }
 
-template <int LC, class Out>
+template <int LC, class Out, int EO = 0>
 __device__ __forceinline__ void store_rows(const cplx* lds, const Out& out, long item, int c0,
                                            int wbits) {
-  using G = Geo<LC>;
+  using G = Geo<LC, EO>;
 #pragma unroll
   for (int k = 0; k < G::EPT; ++k) {
     const int f = threadIdx.x + kNT * k;
@@ -268,10 +279,10 @@ __device__ __forceinline__ void store_rows(const cplx* lds, const Out& out, long
   }
 }
 
-template <int LC, class Out>
+template <int LC, class Out, int EO = 0>
 __device__ __forceinline__ void store_cols(const cplx* lds, const Out& out, long item, int c0,
                                            int wbits) {
-  using G = Geo<LC>;
+  using G = Geo<LC, EO>;
 #pragma unroll
   for (int k = 0; k < G::EPT; ++k) {
     const int f = threadIdx.x + kNT * k;
@@ -280,40 +291,41 @@ __device__ __forceinline__ void store_cols(const cplx* lds, const Out& out, long
   }
 }
 
+// EO: points per thread when given (kPlainEPT: the plain transforms' kp1 / kp2s), else Geo's rule
 // pass 1: columns of [LC][W] (bit-reversed into LDS), stages with the natural table, rows of Z
-template <int LC, class In, class Out>
+template <int LC, class In, class Out, int EO = 0>
 __global__ __launch_bounds__(kNT) void kp1(In in, Out out, int wbits, long nitems,
                                            const cplx* __restrict__ tw1) {
-  using G = Geo<LC>;
+  using G = Geo<LC, EO>;
   extern __shared__ cplx lds[];
   int tile;
   long item;
   tile_item((1 << wbits) / G::T, nitems, &tile, &item);
   const int c0 = tile * G::T;
-  load_cols<LC, true>(lds, in, item, c0, wbits);
+  load_cols<LC, true, In, EO>(lds, in, item, c0, wbits);
   __syncthreads();
   const int cc = threadIdx.x / G::TPC, tl = threadIdx.x % G::TPC;
-  run_stages<LC>(lds + cc * G::CS, tl, tw1);
+  run_stages<LC, 0, G::LOG, EO>(lds + cc * G::CS, tl, tw1);
   __syncthreads();
-  store_rows<LC>(lds, out, item, c0, wbits);
+  store_rows<LC, Out, EO>(lds, out, item, c0, wbits);
 }
 
 // pass 2, natural-order output through Out (the spectrum, or a real row)
-template <int LC, class In, class Out>
+template <int LC, class In, class Out, int EO = 0>
 __global__ __launch_bounds__(kNT) void kp2s(In in, Out out, int wbits, long nitems,
                                             const cplx* __restrict__ tw2) {
-  using G = Geo<LC>;
+  using G = Geo<LC, EO>;
   extern __shared__ cplx lds[];
   int tile;
   long item;
   tile_item((1 << wbits) / G::T, nitems, &tile, &item);
   const int c0 = tile * G::T;
-  load_cols<LC, false>(lds, in, item, c0, wbits);
+  load_cols<LC, false, In, EO>(lds, in, item, c0, wbits);
   __syncthreads();
   const int cc = threadIdx.x / G::TPC, tl = threadIdx.x % G::TPC;
-  run_stages<LC>(lds + cc * G::CS, tl, tw2 + (long)(c0 + cc) * LC);
+  run_stages<LC, 0, G::LOG, EO>(lds + cc * G::CS, tl, tw2 + (long)(c0 + cc) * LC);
   __syncthreads();
-  store_cols<LC>(lds, out, item, c0, wbits);
+  store_cols<LC, Out, EO>(lds, out, item, c0, wbits);
 }
 
 #ifndef JF_KP2R_SCHED

@@ -320,21 +320,24 @@ inline int fft_rows3(long n, bool inverse, long items, In in, Out out, StreamAll
     out_c.p += i0 * out.st;
     st = with_big_lc(tw.A, [&](auto LCc) -> int {
       constexpr int LC = decltype(LCc)::value;
-      return launch_grid<LC>(kp1<LC, In, OutC>, (n / tw.A / Geo<LC>::T) * ni, s, in_c,
-                             OutC{Z, n}, ilog2(n / tw.A), ni, tw.p1);
+      return launch_grid<LC, kPlainEPT<LC>>(kp1<LC, In, OutC, kPlainEPT<LC>>,
+                                            (n / tw.A / PlainGeo<LC>::T) * ni, s, in_c,
+                                            OutC{Z, n}, ilog2(n / tw.A), ni, tw.p1);
     });
     if (st != JW_OK) break;
     st = with_big_lc(tw.B, [&](auto LCc) -> int {
       constexpr int LC = decltype(LCc)::value;
       const Plane pl{Z, n, ab, cbits};
-      return launch_grid<LC>(kp2s<LC, Plane, Plane>, (tw.A / Geo<LC>::T) * ni * tw.C, s, pl, pl,
-                             abits, ni * tw.C, tw.pm);
+      return launch_grid<LC, kPlainEPT<LC>>(kp2s<LC, Plane, Plane, kPlainEPT<LC>>,
+                                            (tw.A / PlainGeo<LC>::T) * ni * tw.C, s, pl, pl,
+                                            abits, ni * tw.C, tw.pm);
     });
     if (st != JW_OK) break;
     st = with_big_lc(tw.C, [&](auto LCc) -> int {
       constexpr int LC = decltype(LCc)::value;
-      return launch_grid<LC>(kp2s<LC, RowsC, Out>, (ab / Geo<LC>::T) * ni, s, RowsC{Z, n}, out_c,
-                             ilog2(ab), ni, tw.p3);
+      return launch_grid<LC, kPlainEPT<LC>>(kp2s<LC, RowsC, Out, kPlainEPT<LC>>,
+                                            (ab / PlainGeo<LC>::T) * ni, s, RowsC{Z, n}, out_c,
+                                            ilog2(ab), ni, tw.p3);
     });
   }
   return st;
@@ -369,14 +372,16 @@ inline int fft_rows(long n, bool inverse, long items, In in, Out out, StreamAllo
     out_c.p += i0 * out.st;
     st = with_big_lc(lc1, [&](auto LCc) -> int {
       constexpr int LC = decltype(LCc)::value;
-      return launch_grid<LC>(kp1<LC, In, OutC>, (lc2 / Geo<LC>::T) * ni, s, in_c, OutC{Z, n},
-                             ilog2(lc2), ni, tw.p1);
+      return launch_grid<LC, kPlainEPT<LC>>(kp1<LC, In, OutC, kPlainEPT<LC>>,
+                                            (lc2 / PlainGeo<LC>::T) * ni, s, in_c, OutC{Z, n},
+                                            ilog2(lc2), ni, tw.p1);
     });
     if (st != JW_OK) break;
     st = with_big_lc(lc2, [&](auto LCc) -> int {
       constexpr int LC = decltype(LCc)::value;
-      return launch_grid<LC>(kp2s<LC, RowsC, Out>, (lc1 / Geo<LC>::T) * ni, s, RowsC{Z, n},
-                             out_c, ilog2(lc1), ni, tw.p2);
+      return launch_grid<LC, kPlainEPT<LC>>(kp2s<LC, RowsC, Out, kPlainEPT<LC>>,
+                                            (lc1 / PlainGeo<LC>::T) * ni, s, RowsC{Z, n},
+                                            out_c, ilog2(lc1), ni, tw.p2);
     });
   }
   return st;
