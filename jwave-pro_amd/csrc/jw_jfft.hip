@@ -319,6 +319,14 @@ int inverse_lines(const ModwtPlan& p, const bool* fft, const cplx* F, const Tw& 
   return JW_OK;
 }
 
+// A/B builds: points per thread of the fused levels' pass-1 kernels (kp1 over real rows) at
+// 512 / 1024 points (0: Geo's rule, 8)
+#ifndef JF_FUSED_P1_EPT
+#define JF_FUSED_P1_EPT 0
+#endif
+template <int LC>
+constexpr int kFusedP1EPT = LC <= 1024 ? JF_FUSED_P1_EPT : 0;
+
 // Column geometry of the level transforms: forward FFTs split N = R x C (pass 1 over columns
 // of length R), inverse FFTs C x R, so every forward pass 2 feeds an inverse pass 1 and every
 // inverse pass 2 a forward pass 1 (jw_jfft.hpp).
@@ -353,8 +361,9 @@ int forward_cols(const ModwtPlan& p, const bool* fft, const cplx* F, const cplx*
     if (!haveZ) {  // forward pass 1 of V_{j-1}
       st = with_big_lc(g.R, [&](auto LCc) -> int {
         constexpr int LC = decltype(LCc)::value;
-        return launch_grid<LC>(kp1<LC, RowsR, OutC>, (g.C / Geo<LC>::T) * nb, s, RowsR{vin, vs},
-                               OutC{Z, N}, g.cbits, nb, twf.p1);
+        constexpr int E = kFusedP1EPT<LC>;
+        return launch_grid<LC, E>(kp1<LC, RowsR, OutC, E>, (g.C / Geo<LC, E>::T) * nb, s,
+                                  RowsR{vin, vs}, OutC{Z, N}, g.cbits, nb, twf.p1);
       });
       if (st != JW_OK) break;
     }
@@ -420,14 +429,15 @@ int inverse_cols(const ModwtPlan& p, const bool* fft, const cplx* F, const cplx*
     }
     st = with_big_lc(g.R, [&](auto LCc) -> int {
       constexpr int LC = decltype(LCc)::value;
-      const long blocks = (g.C / Geo<LC>::T) * nb;
+      constexpr int E = kFusedP1EPT<LC>;
+      const long blocks = (g.C / Geo<LC, E>::T) * nb;
       if (!haveZ) {
-        const int r = launch_grid<LC>(kp1<LC, RowsR, OutC>, blocks, s, RowsR{vin, vs},
-                                      OutC{Zs, N}, g.cbits, nb, twf.p1);
+        const int r = launch_grid<LC, E>(kp1<LC, RowsR, OutC, E>, blocks, s, RowsR{vin, vs},
+                                         OutC{Zs, N}, g.cbits, nb, twf.p1);
         if (r != JW_OK) return r;
       }
-      return launch_grid<LC>(kp1<LC, RowsR, OutC>, blocks, s, RowsR{w, rs}, OutC{Zs + nb * N, N},
-                             g.cbits, nb, twf.p1);
+      return launch_grid<LC, E>(kp1<LC, RowsR, OutC, E>, blocks, s, RowsR{w, rs},
+                                OutC{Zs + nb * N, N}, g.cbits, nb, twf.p1);
     });
     if (st != JW_OK) break;
     st = with_big_lc(g.C, [&](auto LCc) -> int {
