@@ -30,9 +30,12 @@ long bs_m(long n) {
   return m;
 }
 
-// [chirp (n) | B = FFT_m(b) (m)] per (device, n, inverse)
+// [chirp (n) | B = FFT_m(b) (m)] per (device, n, inverse).  Its own budget holds the longest
+// one (n = 2^29: 24 GiB), so repeated long transforms keep their tables: rebuilding means one
+// correctly rounded sin/cos per index on the host (~3 s for n = 3 x 2^25 on 16 threads) -- a
+// table is still kept only while it fits a quarter of the free device memory (cached_table).
 using BsKey = std::tuple<int, long, int>;
-DevCache<BsKey> g_bst(kCacheBytes);
+DevCache<BsKey> g_bst(26UL << 30);
 
 struct BsTab {
   long n = 0, m = 0;
@@ -196,24 +199,25 @@ int bs_conv3(long m, long items, const Pre& pre, const Post& post, const cplx* B
   cplx *Z = nullptr, *Zi = nullptr;
   JW_HIP_TRY(mem.alloc(&Z, (size_t)chunk * m * sizeof(cplx)));
   JW_HIP_TRY(mem.alloc(&Zi, (size_t)chunk * m * sizeof(cplx)));
+  // the passes of fft_rows3, unfused, so with the plain transforms' column geometry (PlainGeo)
   auto three = [&](auto in, auto out, const Tw3& tw, cplx* work, long ni) -> int {
     int r = with_big_lc(tw.A, [&](auto LCc) -> int {
-      constexpr int LC = decltype(LCc)::value;
-      return launch_grid<LC>(kp1<LC, decltype(in), OutC>, (m / tw.A / Geo<LC>::T) * ni, s, in,
-                             OutC{work, m}, ilog2(m / tw.A), ni, tw.p1);
+      constexpr int LC = decltype(LCc)::value, E = kPlainEPT<LC>;
+      return launch_grid<LC, E>(kp1<LC, decltype(in), OutC, E>, (m / tw.A / Geo<LC, E>::T) * ni,
+                                s, in, OutC{work, m}, ilog2(m / tw.A), ni, tw.p1);
     });
     if (r == JW_OK)
       r = with_big_lc(tw.B, [&](auto LCc) -> int {
-        constexpr int LC = decltype(LCc)::value;
+        constexpr int LC = decltype(LCc)::value, E = kPlainEPT<LC>;
         const Plane pl{work, m, ab, cbits};
-        return launch_grid<LC>(kp2s<LC, Plane, Plane>, (tw.A / Geo<LC>::T) * ni * tw.C, s, pl, pl,
-                               abits, ni * tw.C, tw.pm);
+        return launch_grid<LC, E>(kp2s<LC, Plane, Plane, E>, (tw.A / Geo<LC, E>::T) * ni * tw.C,
+                                  s, pl, pl, abits, ni * tw.C, tw.pm);
       });
     if (r == JW_OK)
       r = with_big_lc(tw.C, [&](auto LCc) -> int {
-        constexpr int LC = decltype(LCc)::value;
-        return launch_grid<LC>(kp2s<LC, RowsC, decltype(out)>, (ab / Geo<LC>::T) * ni, s,
-                               RowsC{work, m}, out, ilog2(ab), ni, tw.p3);
+        constexpr int LC = decltype(LCc)::value, E = kPlainEPT<LC>;
+        return launch_grid<LC, E>(kp2s<LC, RowsC, decltype(out), E>, (ab / Geo<LC, E>::T) * ni, s,
+                                  RowsC{work, m}, out, ilog2(ab), ni, tw.p3);
       });
     return r;
   };

@@ -71,9 +71,10 @@ def test_long_pow2_bit_exact_by_last_stage(lg, inverse, device):
         del ref
 
 
-@pytest.mark.parametrize("n", [3 << 26, 3 << 27])
+@pytest.mark.parametrize("n", [3 << 25, 3 << 26, 3 << 27])
 def test_long_bluestein_near_exact(n, device):
-    # m = 2^29, 2^30: the three-pass m-point convolution at its longest (jw_jfft_bs.hip),
+    # m = 2^28, 2^29, 2^30: the three-pass m-point convolution (jw_jfft_bs.hip bs_conv3; 2^28
+    # puts its last pass on 1024-point columns), up to its longest,
     # against torch.fft (exact-twiddle mixed radix on these 3 x 2^k lengths)
     import torch
     gen = torch.Generator(device=device).manual_seed(n)

@@ -362,6 +362,19 @@ def test_bluestein_three_pass_bit_exact(n, knobs):
         assert bits_equal(xr[b], orc.modwt_inverse(ref, g, h, "auto")), b
 
 
+def test_bluestein_three_pass_1024_columns_bit_exact(knobs):
+    # bs_conv3 with m = 2^22 under the lowered switch: split3 gives 1024-point first-pass columns,
+    # run with the plain transforms' geometry (16 points per thread, jw_jfft.hpp kPlainEPT)
+    knobs.setenv("JW_JFFT_3PASS_MIN", str(1 << 18))
+    n = (1 << 20) + 3
+    rng = np.random.default_rng(n)
+    z = rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n)
+    f = FastFourierTransform()
+    X = f.forwardComplex(z)
+    assert bits_equal(X.view(np.float64), orc.fft(z).view(np.float64))
+    assert bits_equal(f.reverseComplex(X).view(np.float64), orc.fft(X, inverse=True).view(np.float64))
+
+
 @pytest.mark.parametrize("n,J", [(1 << 20, 2), (1 << 19, 3)])
 def test_wave_column_kp2p_bit_exact(n, J, knobs):
     # JW_AUTO_WCOL=1 (A/B setting, measured slower, profiles/r06/ab/auto_wcol): the 1024-point
