@@ -168,7 +168,11 @@ namespace {
 // rows [j - 1][0 = h (wavelet), 1 = g (scaling)], natural order; cached per (device, taps, N, J).
 // ---------------------------------------------------------------------------------------
 using SpecKey = std::tuple<int, long, int, std::vector<double>>;
-DevCache<SpecKey> g_spec(kCacheBytes);
+// 2 J N x 16 bytes: 4 GiB for db4 J = 8 at 2^24 -- past a 2 GiB budget every call rebuilt them
+// (the host-wrapped filters and 2 J transforms: 1.23 s per call against ~22 ms, profiles/r06/ab/
+// spectra_cache/), so the budget holds J = 13 at 2^24 (7 GiB); a table is still kept only while
+// it fits a quarter of the free device memory (cached_table)
+DevCache<SpecKey> g_spec(16UL << 30);
 
 // the up-sampled filter of level j (upsample :618-630) wrapped in the reference's order,
 // zero taps included: wrappedFilter[i % N] += filter[i], i ascending
@@ -211,7 +215,7 @@ const cplx* spec_g(const cplx* F, long N, int j) { return F + (long)(2 * (j - 1)
 // F[q][h R + l] (R columns of C points), so that a column's products read consecutive entries.
 // Cached beside F per (device, N, J, taps, R).  env JW_AUTO_SPECT=0: natural order (A/B runs).
 using SpecTKey = std::tuple<int, long, int, long, std::vector<double>>;
-DevCache<SpecTKey> g_spect(kCacheBytes);
+DevCache<SpecTKey> g_spect(16UL << 30);  // the same spectra per kp2p column (two-pass N <= 2^24)
 
 __global__ __launch_bounds__(256) void kspec_t(const cplx* __restrict__ F, cplx* __restrict__ FT,
                                                long N, int rbits, long C) {
